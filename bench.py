@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark: hbbft RBC encode+Merkle (send_shards) at N=64 f=21, 1 MiB proposals.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--instances B]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+A step = one `hbg_rbc_encode_merkle` pass (BE length prefix + pad + chunk +
+RS(22,42) encode + SHA3 Merkle tree) over B resident 1 MiB payloads per GPU
+(BASELINE.json configs[2]).  Instances are sharded across ranks with no
+data-path collective (weak scaling); only the timing max uses a collective.
+`value` = payload bytes of all ranks / max-over-ranks wall time.
+
+Also reported: per-kernel averages (HIP events on the engine's stream),
+the roofline of the dominant kernel (merkle_build: integer-VALU bound, see
+DESIGN.md §Roofline), the decode path (reconstruct 2f erasures + Merkle +
+glue), and the CPU baseline (oracle C port, all host threads, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+N_NODES, PAYLOAD = 64, 1 << 20
+BASE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz; HBM 8 TB/s)
+VALU_PEAK = 256 * 4 * 32 * 2.4e9   # int32 lane-ops/s
+HBM_PEAK = 8.0e12                  # B/s
+# Algorithmic VALU lane-ops: one Keccak-f[1600] on gfx950
+# with 3-input bitop3 + alignbit = 24 rounds x 180; absorbing one 136-B block = 34 xors.
+KECCAK_F_OPS = 24 * 180
+ABSORB_OPS = 34
+
+
+def merkle_counts(N: int, L: int):
+    leaf_perms = N * (L // 136 + 1)
+    pair = 0
+    n = N
+    while n > 1:
+        pair += n // 2
+        n = (n + 1) // 2
+    return leaf_perms, pair
+
+
+def merkle_alg(N: int, L: int):
+    leaf_perms, pair = merkle_counts(N, L)
+    ops = leaf_perms * (KECCAK_F_OPS + ABSORB_OPS) + pair * KECCAK_F_OPS
+    nodes = 2 * N - 1
+    bytes_ = N * L + nodes * 32  # read every shard once, write the flat tree
+    return ops, bytes_
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--instances", type=int, default=2048, help="1 MiB proposals per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=512, help="instances in the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-decode", action="store_true")
+    return ap.parse_args()
+
+
+def timed(fn, reps: int):
+    """Average ms per call of fn over reps (events on the current stream)."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def cpu_baseline(n_sample: int):
+    from oracle import corc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    threads = max(1, min(threads, os.cpu_count() or 1, 64))
+    L = corc.shard_len(N_NODES, PAYLOAD)
+    pay = np.empty((n_sample, PAYLOAD), np.uint8)
+    for k in range(n_sample):
+        pay[k] = corc.synth_bytes(1, k, PAYLOAD)
+    corc.rbc_encode_merkle_batch(N_NODES, pay[:threads], L, threads)  # warm
+    t0 = time.perf_counter()
+    corc.rbc_encode_merkle_batch(N_NODES, pay, L, threads)
+    dt = time.perf_counter() - t0
+    return {"value": n_sample * PAYLOAD / dt / 1e9, "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{n_sample} x 1 MiB send_shards (RS 22+42 AVX2 split-nibble + SHA3 Merkle), "
+                      f"oracle/c/rbc_oracle.c -O3, one instance per thread, {dt:.2f} s wall",
+            "simd": bool(corc.lib().orc_simd_enabled())}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    if dist:
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from hydrabadger_amd import _lib
+    from hydrabadger_amd import broadcast as bc
+
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    ctx = _lib.Context(local)
+    ctx.set_stream(stream.cuda_stream)
+
+    B = a.instances
+    L = _lib.shard_len(N_NODES, PAYLOAD)
+    S = (L + 15) // 16 * 16
+    nodes = _lib.merkle_nodes(N_NODES)
+    data, parity = bc.shard_counts(N_NODES)
+    first = rank * B
+    pay = torch.empty((B, PAYLOAD), dtype=torch.uint8, device=dev)
+    bc.synth_bytes(1, first, PAYLOAD, pay, ctx=ctx, device=True)
+    plen = torch.full((B,), PAYLOAD, dtype=torch.int64, device=dev)
+    shards = torch.empty((B, N_NODES, S), dtype=torch.uint8, device=dev)
+    levels = torch.empty((B, nodes, 32), dtype=torch.uint8, device=dev)
+
+    def step():
+        bc.rbc_encode_merkle_batch(N_NODES, pay, plen, L, shards, levels, ctx=ctx, device=True, asynchronous=True)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    total_bytes = world * B * PAYLOAD * a.steps
+    value = total_bytes / dt / 1e9
+
+    # ---- per-kernel breakdown (rank-local, same stream as the kernels) ----
+    reps = max(3, min(a.steps, 10))
+    ms_merkle = timed(lambda: bc.merkle_build_batch(N_NODES, L, shards, levels, ctx=ctx, device=True,
+                                                     asynchronous=True), reps)
+    ms_step = timed(step, reps)
+    ms_encode = max(ms_step - ms_merkle, 0.0)
+    ops, mbytes = merkle_alg(N_NODES, L)
+    achieved_ops = ops * B / (ms_merkle * 1e-3)
+    enc_bytes = B * (PAYLOAD + N_NODES * L)  # read payload, write N shards
+    roofline = {
+        "kernel": "merkle_build (SHA3-256 leaves + pair tree)",
+        "bound": "valu", "unit": "Tops/s",
+        "achieved": achieved_ops / 1e12, "peak": VALU_PEAK / 1e12, "frac": achieved_ops / VALU_PEAK,
+        "traffic": None,
+        "alg_ops_per_instance": ops, "keccak_f_ops": KECCAK_F_OPS,
+        "hbm": {"achieved_GBps": mbytes * B / (ms_merkle * 1e-3) / 1e9, "peak_GBps": HBM_PEAK / 1e9,
+                "frac": mbytes * B / (ms_merkle * 1e-3) / HBM_PEAK, "alg_bytes_per_instance": mbytes},
+        "avg_ms": ms_merkle, "instances_per_launch": B,
+    }
+    kernels = {"merkle_build_ms": ms_merkle, "rs_encode_const_22_42_ms": ms_encode,
+               "rs_encode_hbm_GBps": enc_bytes / (ms_encode * 1e-3) / 1e9 if ms_encode > 0 else None}
+
+    # ---- decode path: reconstruct exactly 2f erasures + tree + glue ----
+    decode = None
+    if not a.no_decode:
+        from oracle import synth  # seeded erasure masks only (inputs, not the checker)
+        nd = min(B, 512)
+        present = torch.tensor([synth.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
+                               dtype=torch.uint8, device=dev)
+        roots = levels[:nd, nodes - 1, :].contiguous()
+        OS = (data * L + 15) // 16 * 16
+        out = torch.empty((nd, OS), dtype=torch.uint8, device=dev)
+        dplen = torch.empty(nd, dtype=torch.int64, device=dev)
+        st = torch.empty(nd, dtype=torch.uint8, device=dev)
+        work = shards[:nd]
+
+        def dec():
+            bc.rbc_decode_batch(N_NODES, L, work, present, roots, out, dplen, st, ctx=ctx, device=True,
+                                asynchronous=True)
+        dec()
+        torch.cuda.synchronize()
+        ok = bool((st == 1).all().item()) and bool(torch.equal(out[:, :PAYLOAD], pay[:nd]))
+        ms_dec = timed(dec, reps)
+        decode = {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
+                  "erased_per_instance": parity, "roundtrip_ok": ok}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(a.cpu_sample)
+
+    if rank == 0:
+        line = {
+            "metric": BASE["metric"], "value": value, "unit": "GB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (device SplitMix64, seed 0x48424247)",
+            "config": {"workload": "rbc_encode_merkle: send_shards N=64 f=21 (RS 22+42) 1 MiB payloads",
+                       "n_nodes": N_NODES, "f": (N_NODES - 1) // 3, "payload_bytes": PAYLOAD, "shard_len": L,
+                       "instances_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"instances sharded over {world} GPU(s), no data-path collective"},
+            "roofline": roofline, "kernels": kernels, "decode": decode, "cpu_baseline": cpu,
+            "shard_bytes_GBps": value * N_NODES * L / PAYLOAD,
+            "tdec": None,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+"""Build libhbgpu.so (the C-ABI engine) in-tree with hipcc for gfx950.
+
+    python -m hydrabadger_amd.build          # incremental
+    python -m hydrabadger_amd.build --force  # rebuild everything
+
+Objects go to hydrabadger_amd/build/, the library to hydrabadger_amd/libhbgpu.so
+(both git-ignored; the .so travels to the GPU box with gpurun).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(PKG, "build")
+LIB = os.path.join(PKG, "libhbgpu.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("HBG_ARCH", "gfx950")
+CFLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fconstexpr-steps=100000000",
+          "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+
+
+def _deps_mtime(src: str) -> float:
+    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(PKG, "..", "include", "*.h"))
+    return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in hdrs])
+
+
+def _compile(src: str, force: bool) -> str:
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if force or not os.path.exists(obj) or os.path.getmtime(obj) < _deps_mtime(src):
+        cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    print(build(force=a.force))
+    sys.exit(0)

@@ -1,0 +1,511 @@
+// api.hip — C ABI (include/hbgpu.h) over the gfx950 kernels.
+//
+// Host-pointer calls stage through device memory with a padded row stride
+// (S = round_up(L, 16)) using 2-D copies, so the reference's contiguous
+// `send_shards` buffer ([N][L], unpadded) is accepted as-is.  Device-pointer
+// calls (HBG_DEVICE) run in place on the caller's buffers.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "../../include/hbgpu.h"
+#include "gf256.h"
+#include "rbc_kernels.h"
+
+using namespace hbg;
+
+namespace {
+
+constexpr int kNumSlots = 12;
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+}  // namespace
+
+struct hbg_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    Buf slot[kNumSlots];
+    std::map<std::pair<uint32_t, uint32_t>, uint8_t*> matrices;  // device (D+Q) x D coding matrices
+    std::map<std::pair<uint32_t, uint32_t>, uint8_t*> enc_plans; // device shared encode plans
+    std::mutex mu;
+};
+
+namespace {
+
+#define HBG_TRY(expr)                              \
+    do {                                           \
+        hipError_t e_ = (expr);                    \
+        if (e_ != hipSuccess) return HBG_E_DEVICE; \
+    } while (0)
+
+#define HBG_CHECK(expr)              \
+    do {                             \
+        int r_ = (expr);             \
+        if (r_ != HBG_OK) return r_; \
+    } while (0)
+
+uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// Grow-only device scratch slot (synchronises the stream before freeing).
+int scratch(hbg_ctx* c, int i, size_t bytes, void** out) {
+    Buf& b = c->slot[i];
+    if (bytes == 0) bytes = 16;
+    if (b.cap < bytes) {
+        if (b.p) {
+            HBG_TRY(hipStreamSynchronize(c->stream));
+            HBG_TRY(hipFree(b.p));
+            b.p = nullptr;
+            b.cap = 0;
+        }
+        if (hipMalloc(&b.p, bytes) != hipSuccess) return HBG_E_NOMEM;
+        b.cap = bytes;
+    }
+    *out = b.p;
+    return HBG_OK;
+}
+
+int rs_params(uint32_t D, uint32_t Q) {
+    if (D == 0) return HBG_E_TOO_FEW_DATA_SHARDS;
+    if (Q == 0) return HBG_E_TOO_FEW_PARITY_SHARDS;
+    if (D + Q > 256) return HBG_E_TOO_MANY_SHARDS;
+    return HBG_OK;
+}
+
+// rse build_matrix restated on the host (tiny: D^2*(D+Q) GF ops); shipped to
+// the device once per (D, Q).
+void build_matrix_host(uint32_t D, uint32_t Q, uint8_t* out) {
+    const uint32_t N = D + Q;
+    std::vector<uint8_t> top(D * D), inv(D * D), aug(2 * D * D);
+    for (uint32_t r = 0; r < D; ++r)
+        for (uint32_t c = 0; c < D; ++c) top[r * D + c] = gf_pow((uint8_t)r, (int)c);
+    gf_invert(top.data(), (int)D, inv.data(), aug.data());
+    for (uint32_t r = 0; r < N; ++r)
+        for (uint32_t c = 0; c < D; ++c) {
+            uint8_t acc = 0;
+            for (uint32_t t = 0; t < D; ++t) acc ^= gf_mul(gf_pow((uint8_t)r, (int)t), inv[t * D + c]);
+            out[r * D + c] = acc;
+        }
+}
+
+int device_matrix(hbg_ctx* c, uint32_t D, uint32_t Q, uint8_t** out) {
+    auto key = std::make_pair(D, Q);
+    auto it = c->matrices.find(key);
+    if (it != c->matrices.end()) {
+        *out = it->second;
+        return HBG_OK;
+    }
+    std::vector<uint8_t> m((size_t)(D + Q) * D);
+    build_matrix_host(D, Q, m.data());
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, m.size()) != hipSuccess) return HBG_E_NOMEM;
+    HBG_TRY(hipMemcpy(d, m.data(), m.size(), hipMemcpyHostToDevice));
+    c->matrices[key] = d;
+    *out = d;
+    return HBG_OK;
+}
+
+// Shared plan for the generic encoder: outputs D..N-1 from inputs 0..D-1.
+int device_encode_plan(hbg_ctx* c, uint32_t D, uint32_t Q, uint8_t** out) {
+    auto key = std::make_pair(D, Q);
+    auto it = c->enc_plans.find(key);
+    if (it != c->enc_plans.end()) {
+        *out = it->second;
+        return HBG_OK;
+    }
+    const uint64_t ps = plan_stride(D, Q);
+    std::vector<uint8_t> h(ps, 0), m((size_t)(D + Q) * D);
+    build_matrix_host(D, Q, m.data());
+    CodePlan* p = reinterpret_cast<CodePlan*>(h.data());
+    p->status = 0;
+    p->n_out = Q;
+    for (uint32_t j = 0; j < D; ++j) p->in_idx[j] = (uint8_t)j;
+    for (uint32_t k = 0; k < Q; ++k) p->out_idx[k] = (uint8_t)(D + k);
+    memcpy(h.data() + sizeof(CodePlan), m.data() + (size_t)D * D, (size_t)Q * D);
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, ps) != hipSuccess) return HBG_E_NOMEM;
+    HBG_TRY(hipMemcpy(d, h.data(), ps, hipMemcpyHostToDevice));
+    c->enc_plans[key] = d;
+    *out = d;
+    return HBG_OK;
+}
+
+bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p % a) == 0; }
+
+int finish(hbg_ctx* c, uint32_t flags) {
+    if ((flags & HBG_DEVICE) && (flags & HBG_ASYNC)) return HBG_OK;
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+// Encode parity for n instances on a device buffer with row stride S.
+int encode_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t S, uint64_t n,
+                  const uint8_t* payloads, uint64_t pstride, const uint64_t* plen) {
+    if (has_const_encoder(D, Q)) {
+        HBG_TRY(launch_rs_encode_const(D, Q, shards, S, L, n, payloads, pstride, plen, c->stream));
+        return HBG_OK;
+    }
+    if (payloads) HBG_TRY(launch_pack_rows(shards, S, L, D, n, payloads, pstride, plen, c->stream));
+    uint8_t* plan = nullptr;
+    HBG_CHECK(device_encode_plan(c, D, Q, &plan));
+    HBG_TRY(launch_rs_code_generic(shards, S, L, D + Q, D, n, plan, 0, c->stream));
+    return HBG_OK;
+}
+
+int reconstruct_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t S,
+                       const uint8_t* present_dev, uint64_t n, int32_t* status_dev) {
+    uint8_t* mat = nullptr;
+    HBG_CHECK(device_matrix(c, D, Q, &mat));
+    const uint64_t ps = plan_stride(D, Q);
+    void* plans = nullptr;
+    HBG_CHECK(scratch(c, 11, ps * n, &plans));
+    HBG_TRY(launch_rs_plan(present_dev, D, Q, n, mat, (uint8_t*)plans, ps, c->stream));
+    HBG_TRY(launch_rs_code_generic(shards, S, L, D + Q, D, n, (const uint8_t*)plans, ps, c->stream));
+    if (status_dev)
+        HBG_TRY(hipMemcpy2DAsync(status_dev, sizeof(int32_t), plans, ps, sizeof(int32_t), n, hipMemcpyDeviceToDevice,
+                                 c->stream));
+    return HBG_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char* hbg_version(void) { return "hbgpu 0.1 (gfx950)"; }
+
+const char* hbg_strerror(int code) {
+    switch (code) {
+        case HBG_OK: return "ok";
+        case HBG_E_ARG: return "invalid argument";
+        case HBG_E_DEVICE: return "HIP device error";
+        case HBG_E_NOMEM: return "device allocation failed";
+        case HBG_E_TOO_FEW_DATA_SHARDS: return "TooFewDataShards";
+        case HBG_E_TOO_FEW_PARITY_SHARDS: return "TooFewParityShards";
+        case HBG_E_TOO_MANY_SHARDS: return "TooManyShards";
+        case HBG_E_TOO_FEW_SHARDS: return "TooFewShards";
+        case HBG_E_TOO_FEW_SHARDS_PRESENT: return "TooFewShardsPresent";
+        case HBG_E_EMPTY_SHARD: return "EmptyShard";
+        case HBG_E_INCORRECT_SHARD_SIZE: return "IncorrectShardSize";
+        case HBG_E_SINGULAR_MATRIX: return "SingularMatrix";
+        case HBG_E_NOT_ENOUGH_SHARES: return "NotEnoughShares";
+        case HBG_E_DUPLICATE_ENTRY: return "DuplicateEntry";
+        case HBG_E_INVALID_POINT: return "InvalidPoint";
+        default: return "unknown error";
+    }
+}
+
+uint32_t hbg_merkle_nodes(uint32_t n) { return n == 0 ? 1 : merkle_nodes(n); }
+uint32_t hbg_merkle_depth(uint32_t n) { return merkle_depth(n); }
+uint32_t hbg_num_faulty(uint32_t n) { return n == 0 ? 0 : (n - 1) / 3; }
+uint64_t hbg_shard_len(uint32_t n, uint64_t payload_len) {
+    if (n == 0) return 0;
+    const uint32_t D = n - 2 * hbg_num_faulty(n);
+    return (payload_len + 4 + D - 1) / D;
+}
+
+int hbg_coding_matrix(uint32_t data, uint32_t parity, uint8_t* out) {
+    HBG_CHECK(rs_params(data, parity));
+    if (out) build_matrix_host(data, parity, out);
+    return HBG_OK;
+}
+
+int hbg_init(hbg_ctx** out, int device) {
+    if (!out) return HBG_E_ARG;
+    *out = nullptr;
+    int dev = device;
+    if (dev < 0) HBG_TRY(hipGetDevice(&dev));
+    HBG_TRY(hipSetDevice(dev));
+    hbg_ctx* c = new hbg_ctx();
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return HBG_E_DEVICE;
+    }
+    c->stream = c->own;
+    *out = c;
+    return HBG_OK;
+}
+
+void hbg_free(hbg_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& b : c->slot)
+        if (b.p) (void)hipFree(b.p);
+    for (auto& kv : c->matrices) (void)hipFree(kv.second);
+    for (auto& kv : c->enc_plans) (void)hipFree(kv.second);
+    (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int hbg_set_stream(hbg_ctx* c, void* s) {
+    if (!c) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->stream = s ? (hipStream_t)s : c->own;
+    return HBG_OK;
+}
+
+int hbg_sync(hbg_ctx* c) {
+    if (!c) return HBG_E_ARG;
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_rs_encode(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t stride, uint64_t n,
+                  uint32_t flags) {
+    if (!c) return HBG_E_ARG;
+    HBG_CHECK(rs_params(D, Q));
+    if (L == 0) return HBG_E_EMPTY_SHARD;
+    if (stride < L || (n && !shards)) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint32_t N = D + Q;
+    if (flags & HBG_DEVICE) {
+        if (stride % 16 || !aligned(shards, 16)) return HBG_E_ARG;
+        HBG_CHECK(encode_device(c, D, Q, L, shards, stride, n, nullptr, 0, nullptr));
+        return finish(c, flags);
+    }
+    const uint64_t S = round_up(L, 16);
+    void* d = nullptr;
+    HBG_CHECK(scratch(c, 0, S * N * n, &d));
+    HBG_TRY(hipMemcpy2DAsync(d, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_CHECK(encode_device(c, D, Q, L, (uint8_t*)d, S, n, nullptr, 0, nullptr));
+    HBG_TRY(hipMemcpy2DAsync(shards, stride, d, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_rs_reconstruct(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t stride,
+                       const uint8_t* present, int32_t* status, uint64_t n, uint32_t flags) {
+    if (!c) return HBG_E_ARG;
+    HBG_CHECK(rs_params(D, Q));
+    if (L == 0) return HBG_E_EMPTY_SHARD;
+    if (stride < L || (n && (!shards || !present))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint32_t N = D + Q;
+    if (flags & HBG_DEVICE) {
+        if (stride % 16 || !aligned(shards, 16)) return HBG_E_ARG;
+        HBG_CHECK(reconstruct_device(c, D, Q, L, shards, stride, present, n, status));
+        return finish(c, flags);
+    }
+    const uint64_t S = round_up(L, 16);
+    void *d = nullptr, *dp = nullptr, *ds = nullptr;
+    HBG_CHECK(scratch(c, 0, S * N * n, &d));
+    HBG_CHECK(scratch(c, 1, (size_t)N * n, &dp));
+    HBG_CHECK(scratch(c, 2, sizeof(int32_t) * n, &ds));
+    HBG_TRY(hipMemcpy2DAsync(d, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dp, present, (size_t)N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_CHECK(reconstruct_device(c, D, Q, L, (uint8_t*)d, S, (const uint8_t*)dp, n, (int32_t*)ds));
+    HBG_TRY(hipMemcpy2DAsync(shards, stride, d, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
+    std::vector<int32_t> st(n);
+    HBG_TRY(hipMemcpyAsync(st.data(), ds, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    if (status) memcpy(status, st.data(), sizeof(int32_t) * n);
+    return HBG_OK;
+}
+
+int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, uint64_t stride, uint8_t* levels,
+                     uint64_t n, uint32_t flags) {
+    if (!c || N == 0 || N > 256 || stride < L || (n && (!shards || !levels))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint32_t nodes = merkle_nodes(N);
+    if (flags & HBG_DEVICE) {
+        if (stride % 16 || !aligned(shards, 16) || !aligned(levels, 16)) return HBG_E_ARG;
+        HBG_TRY(launch_merkle_build(shards, stride, L, N, n, levels, c->stream));
+        return finish(c, flags);
+    }
+    const uint64_t S = round_up(L, 16);
+    void *d = nullptr, *dl = nullptr;
+    HBG_CHECK(scratch(c, 0, S * N * n, &d));
+    HBG_CHECK(scratch(c, 3, (size_t)nodes * 32 * n, &dl));
+    if (L) HBG_TRY(hipMemcpy2DAsync(d, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(launch_merkle_build((const uint8_t*)d, S, L, N, n, (uint8_t*)dl, c->stream));
+    HBG_TRY(hipMemcpyAsync(levels, dl, (size_t)nodes * 32 * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
+                        const uint32_t* index, const uint8_t* digests, const uint32_t* ndig, const uint8_t* roots,
+                        uint8_t* ok, uint64_t n, uint32_t flags) {
+    if (!c || N == 0 || N > 256 || vstride < len || (n && (!values || !index || !ndig || !roots || !ok)))
+        return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint32_t depth = merkle_depth(N);
+    if (depth && !digests) return HBG_E_ARG;
+    if (flags & HBG_DEVICE) {
+        if (vstride % 16 || !aligned(values, 16)) return HBG_E_ARG;
+        HBG_TRY(launch_merkle_validate(N, len, values, vstride, index, digests, depth, ndig, roots, ok, n,
+                                       c->stream));
+        return finish(c, flags);
+    }
+    const uint64_t S = round_up(len ? len : 1, 16);
+    void *dv, *di, *dd, *dn, *dr, *dok;
+    HBG_CHECK(scratch(c, 0, S * n, &dv));
+    HBG_CHECK(scratch(c, 1, 4 * n, &di));
+    HBG_CHECK(scratch(c, 2, (size_t)32 * depth * n + 16, &dd));
+    HBG_CHECK(scratch(c, 4, 4 * n, &dn));
+    HBG_CHECK(scratch(c, 5, 32 * n, &dr));
+    HBG_CHECK(scratch(c, 6, n, &dok));
+    if (len) HBG_TRY(hipMemcpy2DAsync(dv, S, values, vstride, len, n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(di, index, 4 * n, hipMemcpyHostToDevice, c->stream));
+    if (depth) HBG_TRY(hipMemcpyAsync(dd, digests, (size_t)32 * depth * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dn, ndig, 4 * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dr, roots, 32 * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(launch_merkle_validate(N, len, (const uint8_t*)dv, S, (const uint32_t*)di, (const uint8_t*)dd, depth,
+                                   (const uint32_t*)dn, (const uint8_t*)dr, (uint8_t*)dok, n, c->stream));
+    HBG_TRY(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint64_t pstride,
+                          const uint64_t* plen, uint64_t L, uint8_t* shards, uint64_t stride, uint8_t* levels,
+                          uint64_t n, uint32_t flags) {
+    if (!c || N == 0 || N > 256 || L == 0 || stride < L || (n && (!payloads || !plen || !shards || !levels)))
+        return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint32_t Q = 2 * hbg_num_faulty(N), D = N - Q;
+    const uint32_t nodes = merkle_nodes(N);
+    auto run = [&](const uint8_t* dpay, uint64_t dps, const uint64_t* dplen, uint8_t* dsh, uint64_t S,
+                   uint8_t* dlev) -> int {
+        if (Q) {
+            HBG_CHECK(encode_device(c, D, Q, L, dsh, S, n, dpay, dps, dplen));
+        } else {
+            HBG_TRY(launch_pack_rows(dsh, S, L, N, n, dpay, dps, dplen, c->stream));
+        }
+        HBG_TRY(launch_merkle_build(dsh, S, L, N, n, dlev, c->stream));
+        return HBG_OK;
+    };
+    if (flags & HBG_DEVICE) {
+        if (stride % 16 || !aligned(shards, 16) || !aligned(levels, 16) || pstride % 4 || !aligned(payloads, 4))
+            return HBG_E_ARG;
+        HBG_CHECK(run(payloads, pstride, plen, shards, stride, levels));
+        return finish(c, flags);
+    }
+    uint64_t maxp = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+        if (hbg_shard_len(N, plen[k]) != L || plen[k] > pstride || plen[k] > 0xFFFFFFFFull) return HBG_E_ARG;
+        maxp = plen[k] > maxp ? plen[k] : maxp;
+    }
+    const uint64_t S = round_up(L, 16), PS = round_up(maxp ? maxp : 1, 16);
+    void *dsh, *dpay, *dpl, *dl;
+    HBG_CHECK(scratch(c, 0, S * N * n, &dsh));
+    HBG_CHECK(scratch(c, 1, PS * n, &dpay));
+    HBG_CHECK(scratch(c, 2, 8 * n, &dpl));
+    HBG_CHECK(scratch(c, 3, (size_t)nodes * 32 * n, &dl));
+    if (maxp) HBG_TRY(hipMemcpy2DAsync(dpay, PS, payloads, pstride, maxp, n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dpl, plen, 8 * n, hipMemcpyHostToDevice, c->stream));
+    HBG_CHECK(run((const uint8_t*)dpay, PS, (const uint64_t*)dpl, (uint8_t*)dsh, S, (uint8_t*)dl));
+    HBG_TRY(hipMemcpy2DAsync(shards, stride, dsh, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(levels, dl, (size_t)nodes * 32 * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t stride, const uint8_t* present,
+                   const uint8_t* roots, uint8_t* out, uint64_t ostride, uint64_t* plen, uint8_t* status, uint64_t n,
+                   uint32_t flags) {
+    if (!c || N == 0 || N > 256 || L == 0 || stride < L ||
+        (n && (!shards || !present || !roots || !out || !plen || !status)))
+        return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint32_t Q = 2 * hbg_num_faulty(N), D = N - Q;
+    const uint32_t nodes = merkle_nodes(N);
+    if (ostride < (uint64_t)D * L) return HBG_E_ARG;
+    auto run = [&](uint8_t* dsh, uint64_t S, const uint8_t* dpres, const uint8_t* droots, uint8_t* dout,
+                   uint64_t dos, uint64_t* dplen, uint8_t* dstat) -> int {
+        void *dl = nullptr, *ds = nullptr;
+        HBG_CHECK(scratch(c, 9, (size_t)nodes * 32 * n, &dl));
+        HBG_CHECK(scratch(c, 10, sizeof(int32_t) * n, &ds));
+        if (Q) {
+            HBG_CHECK(reconstruct_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds));
+        } else {
+            // Trivial coding: every shard must be present (hbbft Coding::reconstruct_shards)
+            std::vector<uint8_t> h((size_t)N * n);
+            std::vector<int32_t> st(n);
+            if (flags & HBG_DEVICE) {
+                HBG_TRY(hipMemcpyAsync(h.data(), dpres, h.size(), hipMemcpyDeviceToHost, c->stream));
+                HBG_TRY(hipStreamSynchronize(c->stream));
+            } else {
+                memcpy(h.data(), present, h.size());
+            }
+            for (uint64_t k = 0; k < n; ++k) {
+                st[k] = 0;
+                for (uint32_t i = 0; i < N; ++i)
+                    if (!h[k * N + i]) st[k] = HBG_E_TOO_FEW_SHARDS_PRESENT;
+            }
+            HBG_TRY(hipMemcpyAsync(ds, st.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+        }
+        HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream));
+        HBG_TRY(launch_rbc_glue(dsh, S, L, N, D, n, (const uint8_t*)dl, droots, (const int32_t*)ds, dplen, dstat, dout,
+                                dos, c->stream));
+        return HBG_OK;
+    };
+    if (flags & HBG_DEVICE) {
+        if (stride % 16 || !aligned(shards, 16) || ostride % 4 || !aligned(out, 4)) return HBG_E_ARG;
+        HBG_CHECK(run(shards, stride, present, roots, out, ostride, plen, status));
+        return finish(c, flags);
+    }
+    const uint64_t S = round_up(L, 16), OS = round_up((uint64_t)D * L, 16);
+    void *dsh, *dp, *dr, *dout, *dpl, *dst;
+    HBG_CHECK(scratch(c, 0, S * N * n, &dsh));
+    HBG_CHECK(scratch(c, 1, (size_t)N * n, &dp));
+    HBG_CHECK(scratch(c, 2, 32 * n, &dr));
+    HBG_CHECK(scratch(c, 3, OS * n, &dout));
+    HBG_CHECK(scratch(c, 4, 8 * n, &dpl));
+    HBG_CHECK(scratch(c, 5, n, &dst));
+    HBG_TRY(hipMemcpy2DAsync(dsh, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dp, present, (size_t)N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dr, roots, 32 * n, hipMemcpyHostToDevice, c->stream));
+    HBG_CHECK(run((uint8_t*)dsh, S, (const uint8_t*)dp, (const uint8_t*)dr, (uint8_t*)dout, OS, (uint64_t*)dpl,
+                  (uint8_t*)dst));
+    HBG_TRY(hipMemcpy2DAsync(shards, stride, dsh, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(plen, dpl, 8 * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpy2DAsync(out, ostride, dout, OS, (uint64_t)D * L, n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_synth_bytes(hbg_ctx* c, uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride,
+                    uint64_t n, uint32_t flags) {
+    if (!c || ostride < nbytes || (n && !out)) return HBG_E_ARG;
+    if (n == 0 || nbytes == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    if (flags & HBG_DEVICE) {
+        HBG_TRY(launch_synth(tag, first, nbytes, out, ostride, n, c->stream));
+        return finish(c, flags);
+    }
+    const uint64_t OS = round_up(nbytes, 16);
+    void* d;
+    HBG_CHECK(scratch(c, 0, OS * n, &d));
+    HBG_TRY(launch_synth(tag, first, nbytes, (uint8_t*)d, OS, n, c->stream));
+    HBG_TRY(hipMemcpy2DAsync(out, ostride, d, OS, nbytes, n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,64 @@
+// rbc_kernels.h — launch interface between the C ABI (api.hip) and the
+// gfx950 kernels (rbc_kernels.hip).  Internal; not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hbgpu.h"
+
+namespace hbg {
+
+// Per-instance coding plan consumed by rs_code_generic:
+// out_row[out_idx[o]] = XOR_j coef[o][j] * row[in_idx[j]],  coef follows the
+// struct as [n_out][D] bytes.
+struct CodePlan {
+    int32_t status;  // 0 or HBG_E_*
+    uint32_t n_out;
+    uint8_t in_idx[256];
+    uint8_t out_idx[256];
+};
+
+__host__ __device__ constexpr uint32_t merkle_nodes(uint32_t n) {
+    uint32_t t = 0;
+    while (n > 1) {
+        t += n;
+        n = (n + 1) / 2;
+    }
+    return t + 1;
+}
+
+__host__ __device__ constexpr uint32_t merkle_depth(uint32_t n) {
+    uint32_t d = 0;
+    while (n > 1) {
+        n = (n + 1) / 2;
+        ++d;
+    }
+    return d;
+}
+
+inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
+    return (sizeof(CodePlan) + (uint64_t)max_out * D + 15) & ~uint64_t(15);
+}
+
+bool has_const_encoder(uint32_t D, uint32_t Q);
+hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                  const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
+hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
+                            const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
+hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
+                                  const uint8_t* plans, uint64_t plan_stride, hipStream_t st);
+hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint64_t n, const uint8_t* matrix,
+                          uint8_t* plans, uint64_t plan_stride, hipStream_t st);
+hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
+                               uint8_t* levels, hipStream_t st);
+hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
+                                  const uint32_t* index, const uint8_t* digests, uint32_t depth,
+                                  const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
+                                  hipStream_t st);
+hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
+                           const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
+                           uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st);
+hipError_t launch_synth(uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride, uint64_t n,
+                        hipStream_t st);
+
+}  // namespace hbg

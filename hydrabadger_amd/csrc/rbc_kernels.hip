@@ -1,0 +1,536 @@
+// rbc_kernels.hip — gfx950 kernels for hbbft's reliable-broadcast coding path.
+//
+// Families:
+//   1. GF(2^8) coding    rs_encode_const<D,Q>  (a2+a3: Coding::encode, optionally
+//                        fused with send_shards' length-prefix/pad/chunk), rs_code_generic
+//                        (any matrix: encode for other (D,Q), reconstruct), rs_plan
+//                        (a7: first-D-present inverse per instance)
+//   2. Keccak/Merkle     merkle_build (a4: MerkleTree::from_vec, levels + root),
+//                        merkle_validate (a6: Proof::validate)
+//   glue                 rbc_glue_status / rbc_glue_copy (a8: glue_shards + root check),
+//                        synth_bytes (seeded inputs)
+//
+// Device layout: instance k, shard i at
+//   shards + (k*N + i)*S,  S % 16 == 0,  L meaningful bytes, [L, S) scratch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "gf256.h"
+#include "keccak.h"
+#include "rbc_kernels.h"
+
+namespace hbg {
+
+// ============================================================== family 1: coding
+// Value byte x of an instance (send_shards' buffer): BE u32 length || payload || zeros.
+__device__ __forceinline__ uint32_t value_byte(const uint8_t* __restrict__ pay, uint64_t P, uint64_t x) {
+    if (x < 4) return (uint32_t)((P >> (8 * (3 - x))) & 0xFF);
+    return (x - 4 < P) ? pay[x - 4] : 0u;
+}
+
+// 4 value bytes [v, v+4) packed little-endian.  `pay` is 4-byte aligned and
+// any 32-bit word holding a byte < P is readable.
+__device__ __forceinline__ uint32_t value_word(const uint8_t* __restrict__ pay, uint64_t P, uint64_t v) {
+    if (v >= 4 && v + 4 <= P + 4) {
+        const uint64_t o = v - 4;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(pay) + (o >> 2);
+        const uint32_t s = (uint32_t)(o & 3);
+        const uint32_t w0 = w[0];
+        const uint32_t w1 = s ? w[1] : 0u;
+        return __builtin_amdgcn_alignbyte(w1, w0, s);
+    }
+    if (v >= P + 4) return 0u;
+    return value_byte(pay, P, v) | (value_byte(pay, P, v + 1) << 8) | (value_byte(pay, P, v + 2) << 16) |
+           (value_byte(pay, P, v + 3) << 24);
+}
+
+template <int D, int Q, int J, int... K>
+__device__ __forceinline__ void mac_column(uint32_t (&acc)[Q], const Pow8& P, std::integer_sequence<int, K...>) {
+    ((acc[K] = cmul_acc<kParity<D, Q>.m[K][J]>(acc[K], P)), ...);
+}
+
+template <int D, int Q, bool FROM_PAYLOAD, int J>
+__device__ __forceinline__ void encode_column(uint32_t (&acc)[Q], uint8_t* __restrict__ inst_base, uint64_t S,
+                                              uint64_t L, uint32_t p, const uint8_t* __restrict__ pay,
+                                              uint64_t P) {
+    uint32_t* row = reinterpret_cast<uint32_t*>(inst_base + (uint64_t)J * S);
+    uint32_t w;
+    if constexpr (FROM_PAYLOAD) {
+        w = value_word(pay, P, (uint64_t)J * L + 4 * (uint64_t)p);
+        row[p] = w;
+    } else {
+        w = row[p];
+    }
+    const Pow8 pw = powers(w);
+    mac_column<D, Q, J>(acc, pw, std::make_integer_sequence<int, Q>{});
+}
+
+template <int D, int Q, bool FROM_PAYLOAD, int... J>
+__device__ __forceinline__ void encode_all(uint32_t (&acc)[Q], uint8_t* __restrict__ inst_base, uint64_t S,
+                                           uint64_t L, uint32_t p, const uint8_t* __restrict__ pay, uint64_t P,
+                                           std::integer_sequence<int, J...>) {
+    (encode_column<D, Q, FROM_PAYLOAD, J>(acc, inst_base, S, L, p, pay, P), ...);
+}
+
+// One thread = 4 byte positions of one instance, all N shards.
+template <int D, int Q, bool FROM_PAYLOAD>
+__global__ __launch_bounds__(256) void rs_encode_const(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+                                                       uint64_t n, uint32_t blocks_per_inst,
+                                                       const uint8_t* __restrict__ payloads, uint64_t pstride,
+                                                       const uint64_t* __restrict__ plen) {
+    const uint64_t inst = blockIdx.x / blocks_per_inst;
+    const uint32_t p = (blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
+    if (inst >= n || 4 * (uint64_t)p >= L) return;
+    uint8_t* base = shards + inst * (uint64_t)(D + Q) * S;
+    const uint8_t* pay = nullptr;
+    uint64_t P = 0;
+    if constexpr (FROM_PAYLOAD) {
+        pay = payloads + inst * pstride;
+        P = plen[inst];
+    }
+    uint32_t acc[Q];
+#pragma unroll
+    for (int k = 0; k < Q; ++k) acc[k] = 0u;
+    encode_all<D, Q, FROM_PAYLOAD>(acc, base, S, L, p, pay, P, std::make_integer_sequence<int, D>{});
+#pragma unroll
+    for (int k = 0; k < Q; ++k) reinterpret_cast<uint32_t*>(base + (uint64_t)(D + k) * S)[p] = acc[k];
+}
+
+// Pack only (Trivial coding, N <= 3): send_shards' buffer into N rows.
+__global__ __launch_bounds__(256) void pack_rows(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint32_t N,
+                                                 uint64_t n, uint32_t blocks_per_inst,
+                                                 const uint8_t* __restrict__ payloads, uint64_t pstride,
+                                                 const uint64_t* __restrict__ plen) {
+    const uint64_t inst = blockIdx.x / blocks_per_inst;
+    const uint64_t p = (uint64_t)(blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
+    if (inst >= n || 4 * p >= L) return;
+    const uint8_t* pay = payloads + inst * pstride;
+    const uint64_t P = plen[inst];
+    for (uint32_t j = 0; j < N; ++j)
+        reinterpret_cast<uint32_t*>(shards + (inst * N + j) * S)[p] = value_word(pay, P, (uint64_t)j * L + 4 * p);
+}
+
+// Generic coding: out_row[o] = XOR_j coef[o][j] * in_row[j] for one instance's
+// plan (see rbc_kernels.h CodePlan).  Output tile of 32 rows in registers.
+constexpr int kGenericTile = 32;
+
+__global__ __launch_bounds__(256) void rs_code_generic(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+                                                       uint32_t N, uint32_t D, uint64_t n,
+                                                       uint32_t blocks_per_inst, const uint8_t* __restrict__ plans,
+                                                       uint64_t plan_stride) {
+    const uint64_t inst = blockIdx.x / blocks_per_inst;
+    const uint32_t p = (blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
+    if (inst >= n) return;
+    const CodePlan* plan = reinterpret_cast<const CodePlan*>(plans + inst * plan_stride);
+    if (plan->status != 0 || 4 * (uint64_t)p >= L) return;
+    const uint32_t n_out = plan->n_out;
+    const uint8_t* coef = reinterpret_cast<const uint8_t*>(plan) + sizeof(CodePlan);
+    uint8_t* base = shards + inst * (uint64_t)N * S;
+    for (uint32_t o0 = 0; o0 < n_out; o0 += kGenericTile) {
+        uint32_t acc[kGenericTile];
+#pragma unroll
+        for (int o = 0; o < kGenericTile; ++o) acc[o] = 0u;
+        const uint32_t cnt = (n_out - o0) < (uint32_t)kGenericTile ? (n_out - o0) : (uint32_t)kGenericTile;
+        for (uint32_t j = 0; j < D; ++j) {
+            const uint32_t w = reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p];
+            const Pow8 pw = powers(w);
+#pragma unroll
+            for (int o = 0; o < kGenericTile; ++o)
+                if ((uint32_t)o < cnt) acc[o] ^= rmul(coef[(o0 + o) * D + j], pw);
+        }
+#pragma unroll
+        for (int o = 0; o < kGenericTile; ++o)
+            if ((uint32_t)o < cnt)
+                reinterpret_cast<uint32_t*>(base + (uint64_t)plan->out_idx[o0 + o] * S)[p] = acc[o];
+    }
+}
+
+// Per-instance reconstruct plan (rse reconstruct_internal, restated):
+// rows_used = first D present rows in index order; dec = inv(M[rows_used]);
+// for every missing row r: coef[r] = M[r] * dec (so one pass rebuilds missing
+// data AND parity rows; identical bytes to rse's two-pass form because both
+// are the same linear map of the same D input rows).
+// One 256-thread workgroup per instance; dynamic LDS: aug[D][2D] + row buffer.
+__global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ present, uint32_t D, uint32_t Q,
+                                               uint64_t n, const uint8_t* __restrict__ matrix,
+                                               uint8_t* __restrict__ plans, uint64_t plan_stride) {
+    const uint64_t inst = blockIdx.x;
+    if (inst >= n) return;
+    const uint32_t N = D + Q;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* lg = lds;           // 256
+    uint8_t* ex = lds + 256;     // 512
+    uint8_t* aug = lds + 768;    // D * 2D
+    __shared__ uint32_t s_rows[256];
+    __shared__ uint32_t s_np, s_nout, s_status, s_piv;
+    __shared__ uint8_t s_out[256];
+    const uint8_t* pr = present + inst * N;
+    CodePlan* plan = reinterpret_cast<CodePlan*>(plans + inst * plan_stride);
+    uint8_t* coef = reinterpret_cast<uint8_t*>(plan) + sizeof(CodePlan);
+    const uint32_t t = threadIdx.x;
+    // GF tables into LDS
+    for (uint32_t i = t; i < 256; i += blockDim.x) lg[i] = kGf.log[i];
+    for (uint32_t i = t; i < 510; i += blockDim.x) ex[i] = kGf.exp[i];
+    if (t == 0) {
+        uint32_t np = 0, no = 0;
+        for (uint32_t i = 0; i < N; ++i) {
+            if (pr[i]) {
+                if (np < D) s_rows[np] = i;
+                ++np;
+            } else {
+                s_out[no++] = (uint8_t)i;
+            }
+        }
+        s_np = np;
+        s_nout = no;
+        s_status = (np < D) ? (uint32_t)(-HBG_E_TOO_FEW_SHARDS_PRESENT) : 0u;
+    }
+    __syncthreads();
+    auto gmul = [&](uint32_t a, uint32_t b) -> uint32_t { return (a && b) ? ex[lg[a] + lg[b]] : 0u; };
+    if (s_status != 0 || s_nout == 0) {
+        if (t == 0) {
+            plan->status = s_status ? -(int32_t)s_status : 0;
+            plan->n_out = 0;
+        }
+        return;
+    }
+    // aug = [M[rows_used] | I]
+    const uint32_t W = 2 * D;
+    for (uint32_t e = t; e < D * W; e += blockDim.x) {
+        const uint32_t r = e / W, c = e % W;
+        aug[e] = c < D ? matrix[s_rows[r] * D + c] : (uint8_t)(c - D == r);
+    }
+    __syncthreads();
+    for (uint32_t r = 0; r < D; ++r) {
+        if (t == 0) {
+            uint32_t piv = r;
+            while (piv < D && aug[piv * W + r] == 0) ++piv;
+            s_piv = piv;
+        }
+        __syncthreads();
+        const uint32_t piv = s_piv;
+        if (piv == D) {  // singular: cannot happen for a Vandermonde-derived M
+            if (t == 0) {
+                plan->status = HBG_E_SINGULAR_MATRIX;
+                plan->n_out = 0;
+            }
+            return;
+        }
+        if (piv != r)
+            for (uint32_t c = t; c < W; c += blockDim.x) {
+                const uint8_t a = aug[r * W + c];
+                aug[r * W + c] = aug[piv * W + c];
+                aug[piv * W + c] = a;
+            }
+        __syncthreads();
+        const uint32_t s = ex[255 - lg[aug[r * W + r]]];  // inverse of pivot (log of 1 = 0 -> exp[255] = 1)
+        __syncthreads();
+        for (uint32_t c = t; c < W; c += blockDim.x) aug[r * W + c] = (uint8_t)gmul(s, aug[r * W + c]);
+        __syncthreads();
+        for (uint32_t e = t; e < D * W; e += blockDim.x) {
+            const uint32_t rb = e / W, c = e % W;
+            if (rb == r) continue;
+            const uint32_t f = aug[rb * W + r];
+            if (f && c != r) aug[e] ^= (uint8_t)gmul(f, aug[r * W + c]);
+        }
+        __syncthreads();
+        for (uint32_t rb = t; rb < D; rb += blockDim.x)
+            if (rb != r) aug[rb * W + r] = 0;
+        __syncthreads();
+    }
+    // coef[o][c] = sum_t M[out_o][t] * dec[t][c],  dec[t][c] = aug[t*W + D + c]
+    const uint32_t no = s_nout;
+    for (uint32_t e = t; e < no * D; e += blockDim.x) {
+        const uint32_t o = e / D, c = e % D;
+        const uint8_t* mrow = matrix + (uint32_t)s_out[o] * D;
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < D; ++k) acc ^= gmul(mrow[k], aug[k * W + D + c]);
+        coef[o * D + c] = (uint8_t)acc;
+    }
+    for (uint32_t j = t; j < D; j += blockDim.x) plan->in_idx[j] = (uint8_t)s_rows[j];
+    for (uint32_t o = t; o < no; o += blockDim.x) plan->out_idx[o] = s_out[o];
+    if (t == 0) {
+        plan->status = 0;
+        plan->n_out = no;
+    }
+}
+
+// ============================================================== family 2: Merkle
+// One work-item per leaf; lanes_per_inst = next_pow2(N) (<= 256); tree levels
+// built in LDS by the owning lanes.  levels: [n][nodes][32].
+__global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+                                                    uint32_t N, uint32_t lpi, uint32_t nodes, uint64_t n,
+                                                    uint8_t* __restrict__ levels) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t mlds[];
+    const uint32_t ipb = 256 / lpi;
+    const uint32_t li = threadIdx.x / lpi, leaf = threadIdx.x % lpi;
+    const uint64_t inst = (uint64_t)blockIdx.x * ipb + li;
+    const bool live = inst < n;
+    uint32_t* tree = mlds + (uint64_t)li * nodes * 8;
+    uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)nodes * 32);
+    if (live && leaf < N) {
+        uint32_t d[8];
+        sha3_256_aligned8(shards + (inst * N + leaf) * S, L, d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tree[leaf * 8 + i] = d[i];
+        gout[2 * leaf] = make_uint4(d[0], d[1], d[2], d[3]);
+        gout[2 * leaf + 1] = make_uint4(d[4], d[5], d[6], d[7]);
+    }
+    __syncthreads();
+    uint32_t base = 0, cnt = N;
+    while (cnt > 1) {
+        const uint32_t nn = (cnt + 1) / 2;
+        if (live && leaf < nn) {
+            uint32_t d[8];
+            if (2 * leaf + 1 < cnt) {
+                uint32_t l[8], r[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    l[i] = tree[(base + 2 * leaf) * 8 + i];
+                    r[i] = tree[(base + 2 * leaf + 1) * 8 + i];
+                }
+                sha3_pair(l, r, d);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) d[i] = tree[(base + 2 * leaf) * 8 + i];
+            }
+            const uint32_t at = base + cnt + leaf;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tree[at * 8 + i] = d[i];
+            gout[2 * at] = make_uint4(d[0], d[1], d[2], d[3]);
+            gout[2 * at + 1] = make_uint4(d[4], d[5], d[6], d[7]);
+        }
+        __syncthreads();
+        base += cnt;
+        cnt = nn;
+    }
+}
+
+// Proof::validate(N) — one work-item per proof.
+__global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len, const uint8_t* __restrict__ values,
+                                                       uint64_t vstride, const uint32_t* __restrict__ index,
+                                                       const uint8_t* __restrict__ digests, uint32_t depth,
+                                                       const uint32_t* __restrict__ ndig,
+                                                       const uint8_t* __restrict__ roots, uint8_t* __restrict__ ok,
+                                                       uint64_t n) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint32_t d[8];
+    sha3_256_aligned8(values + k * vstride, len, d);
+    uint32_t li = index[k], ln = N, used = 0;
+    const uint32_t nd = ndig[k];
+    const uint32_t* dg = reinterpret_cast<const uint32_t*>(digests + k * (uint64_t)depth * 32);
+    bool good = true;
+    while (ln > 1) {
+        if ((li ^ 1u) < ln) {
+            if (used >= nd || used >= depth) {
+                good = false;
+                break;
+            }
+            uint32_t s[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s[i] = dg[used * 8 + i];
+            ++used;
+            if (li & 1u) sha3_pair(s, d, d);
+            else sha3_pair(d, s, d);
+        }
+        li >>= 1;
+        ln = (ln + 1) >> 1;
+    }
+    if (good && used != nd) good = false;
+    if (good) {
+        const uint32_t* rt = reinterpret_cast<const uint32_t*>(roots + k * 32);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) good &= (rt[i] == d[i]);
+    }
+    ok[k] = good ? 1 : 0;
+}
+
+// ============================================================== glue (a8)
+// status/length per instance: root check + BE u32 length of the glued value.
+__global__ void rbc_glue_status(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D,
+                                uint64_t n, const uint8_t* __restrict__ levels, uint32_t nodes,
+                                const uint8_t* __restrict__ roots, const int32_t* __restrict__ rstatus,
+                                uint64_t* __restrict__ plen, uint8_t* __restrict__ status) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    bool good = rstatus ? (rstatus[k] == 0) : true;
+    if (good) {
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(levels + (k * nodes + nodes - 1) * 32);
+        const uint32_t* b = reinterpret_cast<const uint32_t*>(roots + k * 32);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) good &= (a[i] == b[i]);
+    }
+    const uint64_t tot = (uint64_t)D * L;
+    if (good && tot < 4) good = false;
+    uint64_t len = 0;
+    if (good) {
+        const uint8_t* inst = shards + k * N * S;
+        uint32_t v = 0;
+        for (uint32_t x = 0; x < 4; ++x) v = (v << 8) | inst[(x / L) * S + x % L];
+        len = v;
+        if (len > tot - 4) len = tot - 4;  // `take(len)` truncates silently
+    }
+    plen[k] = len;
+    status[k] = good ? HBG_DECODE_OK : HBG_DECODE_NONE;
+}
+
+// payload byte q = value byte q+4; thread per output word.
+__global__ __launch_bounds__(256) void rbc_glue_copy(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+                                                     uint32_t N, uint64_t n, uint32_t blocks_per_inst,
+                                                     const uint64_t* __restrict__ plen,
+                                                     const uint8_t* __restrict__ status, uint8_t* __restrict__ out,
+                                                     uint64_t ostride) {
+    const uint64_t inst = blockIdx.x / blocks_per_inst;
+    const uint64_t q = ((uint64_t)(blockIdx.x % blocks_per_inst) * 256 + threadIdx.x) * 4;
+    if (inst >= n || status[inst] != HBG_DECODE_OK) return;
+    const uint64_t len = plen[inst];
+    if (q >= len) return;
+    const uint8_t* base = shards + inst * N * S;
+    const uint32_t Lw = (uint32_t)L;
+    const uint32_t x = (uint32_t)(q + 4);
+    const uint32_t r = x / Lw, c = x - r * Lw;
+    uint32_t w;
+    if (c + 4 <= Lw) {
+        const uint8_t* rowp = base + (uint64_t)r * S;
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(rowp) + (c >> 2);
+        const uint32_t s = c & 3;
+        const uint32_t w0 = pw[0];
+        const uint32_t w1 = s ? pw[1] : 0u;
+        w = __builtin_amdgcn_alignbyte(w1, w0, s);
+    } else {
+        w = 0;
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t xb = x + b, rb = xb / Lw, cb = xb - rb * Lw;
+            w |= (uint32_t)base[(uint64_t)rb * S + cb] << (8 * b);
+        }
+    }
+    uint8_t* dst = out + inst * ostride + q;
+    if (q + 4 <= len) {
+        *reinterpret_cast<uint32_t*>(dst) = w;  // ostride % 4 == 0
+    } else {
+        for (uint64_t b = 0; q + b < len; ++b) dst[b] = (uint8_t)(w >> (8 * b));
+    }
+}
+
+// ============================================================== synthetic inputs
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_bytes(uint32_t tag, uint64_t first, uint64_t nbytes,
+                                                   uint8_t* __restrict__ out, uint64_t ostride, uint64_t n,
+                                                   uint32_t blocks_per_row) {
+    const uint64_t row = blockIdx.x / blocks_per_row;
+    const uint64_t w = (uint64_t)(blockIdx.x % blocks_per_row) * 256 + threadIdx.x;
+    if (row >= n || 8 * w >= nbytes) return;
+    const uint64_t seed = 0x48424247ull ^ ((uint64_t)tag << 48) ^ (first + row);
+    const uint64_t v = mix64(seed + (w + 1) * 0x9E3779B97F4A7C15ull);
+    uint8_t* dst = out + row * ostride + 8 * w;
+    if (8 * w + 8 <= nbytes && (ostride % 8) == 0) {
+        *reinterpret_cast<uint64_t*>(dst) = v;
+    } else {
+        for (uint64_t b = 0; b < 8 && 8 * w + b < nbytes; ++b) dst[b] = (uint8_t)(v >> (8 * b));
+    }
+}
+
+// ============================================================== launchers
+template <int D, int Q>
+static hipError_t launch_encode_const(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                      const uint8_t* payloads, uint64_t pstride, const uint64_t* plen,
+                                      hipStream_t st) {
+    const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    const uint64_t blocks = n * bpi;
+    if (payloads)
+        rs_encode_const<D, Q, true><<<dim3((uint32_t)blocks), dim3(256), 0, st>>>(shards, S, L, n, bpi, payloads,
+                                                                                   pstride, plen);
+    else
+        rs_encode_const<D, Q, false><<<dim3((uint32_t)blocks), dim3(256), 0, st>>>(shards, S, L, n, bpi, nullptr, 0,
+                                                                                    nullptr);
+    return hipGetLastError();
+}
+
+bool has_const_encoder(uint32_t D, uint32_t Q) {
+    return (D == 2 && Q == 2) || (D == 6 && Q == 10) || (D == 22 && Q == 42) || (D == 44 && Q == 84);
+}
+
+hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                  const uint8_t* payloads, uint64_t pstride, const uint64_t* plen,
+                                  hipStream_t st) {
+    if (D == 2 && Q == 2) return launch_encode_const<2, 2>(shards, S, L, n, payloads, pstride, plen, st);
+    if (D == 6 && Q == 10) return launch_encode_const<6, 10>(shards, S, L, n, payloads, pstride, plen, st);
+    if (D == 22 && Q == 42) return launch_encode_const<22, 42>(shards, S, L, n, payloads, pstride, plen, st);
+    if (D == 44 && Q == 84) return launch_encode_const<44, 84>(shards, S, L, n, payloads, pstride, plen, st);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
+                            const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st) {
+    const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    pack_rows<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, payloads, pstride, plen);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
+                                  const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
+    const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    rs_code_generic<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, D, n, bpi, plans,
+                                                                      plan_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint64_t n, const uint8_t* matrix,
+                          uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
+    const size_t lds = 768 + (size_t)D * 2 * D;
+    rs_plan<<<dim3((uint32_t)n), dim3(256), lds, st>>>(present, D, Q, n, matrix, plans, plan_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
+                               uint8_t* levels, hipStream_t st) {
+    uint32_t lpi = 1;
+    while (lpi < N) lpi <<= 1;
+    const uint32_t nodes = merkle_nodes(N);
+    const uint32_t ipb = 256 / lpi;
+    const uint64_t blocks = (n + ipb - 1) / ipb;
+    const size_t lds = (size_t)ipb * nodes * 32;
+    merkle_build<<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
+    return hipGetLastError();
+}
+
+hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
+                                  const uint32_t* index, const uint8_t* digests, uint32_t depth,
+                                  const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
+                                  hipStream_t st) {
+    merkle_validate<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index, digests,
+                                                                            depth, ndig, roots, ok, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
+                           const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
+                           uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st) {
+    const uint32_t nodes = merkle_nodes(N);
+    rbc_glue_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(shards, S, L, N, D, n, levels, nodes,
+                                                                            roots, rstatus, plen, status);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t maxlen = (uint64_t)D * L;
+    const uint32_t bpi = (uint32_t)(((maxlen + 3) / 4 + 255) / 256);
+    rbc_glue_copy<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, plen, status, out,
+                                                                    ostride);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride, uint64_t n,
+                        hipStream_t st) {
+    const uint32_t bpr = (uint32_t)(((nbytes + 7) / 8 + 255) / 256);
+    synth_bytes<<<dim3((uint32_t)(n * bpr)), dim3(256), 0, st>>>(tag, first, nbytes, out, ostride, n, bpr);
+    return hipGetLastError();
+}
+
+}  // namespace hbg

@@ -1,0 +1,144 @@
+/* hbgpu.h — C ABI of the MI355X (gfx950) batch engine for hbbft's RBC coding,
+ * Merkle and ThresholdDecrypt hot path, as driven by hydrabadger.
+ *
+ * The reference (VegeBun-csj/hydrabadger) reaches this path only through hbbft:
+ *   propose         /root/reference/src/hydrabadger/state.rs:484  dhb.propose(contrib, rng)
+ *   handle_message  /root/reference/src/hydrabadger/state.rs:486-487 dhb.handle_message(src, msg, rng)
+ * and, inside hbbft [EXT, VegeBun-csj/hbbft master, unvendored], through the
+ * call surfaces each entry point below replaces.  Every
+ * entry point is batch-first: a single hbbft call is n = 1.
+ *
+ * Conventions
+ *  - Return 0 (HBG_OK) or a negative HBG_E_* code.  Per-instance outcomes
+ *    (hbbft's `None` / `false`) go to per-item status/ok arrays.
+ *  - flags & HBG_DEVICE: every buffer argument (including small metadata
+ *    arrays) is a device pointer on the context's device; otherwise all are
+ *    host pointers and the engine stages them through device memory.
+ *  - flags & HBG_ASYNC (device mode only): return after enqueueing on the
+ *    context stream; call hbg_sync().  Without it calls are synchronous.
+ *  - Shard batches: instance k's shard i starts at
+ *        shards + (k * N + i) * shard_stride
+ *    and holds shard_len (L) meaningful bytes.  Host mode accepts any
+ *    shard_stride >= L (shard_stride == L is the reference's own contiguous
+ *    `send_shards` buffer).  Device mode needs shard_stride % 16 == 0 and a
+ *    16-byte-aligned base; bytes [L, shard_stride) of each row are engine
+ *    scratch (they may be overwritten; they are never hashed).
+ *  - Merkle trees are returned as the flat digest array of hbbft's
+ *    `MerkleTree.levels` followed by the root: [nodes][32] per instance with
+ *    nodes = hbg_merkle_nodes(N); level l (size n_l, n_0 = N,
+ *    n_{l+1} = ceil(n_l/2)) starts at sum_{m<l} n_m; the root is the last
+ *    digest.  `MerkleTree::proof(i)` is a pure index walk over this array.
+ *  - No callbacks; no allocation is returned to the caller.
+ */
+#ifndef HBGPU_H
+#define HBGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes (mirror rse::Error / threshold_crypto::Error variants) ---- */
+#define HBG_OK 0
+#define HBG_E_ARG (-1)                    /* bad argument / alignment / layout        */
+#define HBG_E_DEVICE (-2)                 /* HIP runtime failure                      */
+#define HBG_E_NOMEM (-3)                  /* device allocation failed                 */
+#define HBG_E_TOO_FEW_DATA_SHARDS (-10)   /* rse::Error::TooFewDataShards             */
+#define HBG_E_TOO_FEW_PARITY_SHARDS (-11) /* rse::Error::TooFewParityShards           */
+#define HBG_E_TOO_MANY_SHARDS (-12)       /* rse::Error::TooManyShards                */
+#define HBG_E_TOO_FEW_SHARDS (-13)        /* rse::Error::TooFewShards                 */
+#define HBG_E_TOO_FEW_SHARDS_PRESENT (-14)/* rse::Error::TooFewShardsPresent          */
+#define HBG_E_EMPTY_SHARD (-15)           /* rse::Error::EmptyShard                   */
+#define HBG_E_INCORRECT_SHARD_SIZE (-16)  /* rse::Error::IncorrectShardSize           */
+#define HBG_E_SINGULAR_MATRIX (-17)       /* rse::Error::SingularMatrix (internal)    */
+#define HBG_E_NOT_ENOUGH_SHARES (-20)     /* threshold_crypto::Error::NotEnoughShares */
+#define HBG_E_DUPLICATE_ENTRY (-21)       /* threshold_crypto::Error::DuplicateEntry  */
+#define HBG_E_INVALID_POINT (-22)         /* bad compressed G1/G2 encoding            */
+
+#define HBG_DEVICE 1u
+#define HBG_ASYNC 2u
+
+/* per-instance decode status (hbg_rbc_decode) */
+#define HBG_DECODE_OK 1          /* Some(payload)                                  */
+#define HBG_DECODE_NONE 0        /* None: too few shards, root mismatch or < 4 B   */
+
+typedef struct hbg_ctx hbg_ctx;
+
+/* ---- context ---- */
+int hbg_init(hbg_ctx **out, int device); /* device < 0: the current HIP device */
+void hbg_free(hbg_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int hbg_set_stream(hbg_ctx *ctx, void *hip_stream);
+int hbg_sync(hbg_ctx *ctx);
+const char *hbg_strerror(int code);
+const char *hbg_version(void);
+
+/* ---- shape helpers (pure host functions) ---- */
+uint32_t hbg_merkle_nodes(uint32_t n);                /* digests in a flat tree    */
+uint32_t hbg_merkle_depth(uint32_t n);                /* max digests in a proof    */
+uint32_t hbg_num_faulty(uint32_t n);                  /* hbbft NetworkInfo: (N-1)/3 */
+uint64_t hbg_shard_len(uint32_t n, uint64_t payload_len); /* ceil((P+4)/(N-2f))     */
+
+/* Coding::new(data, parity) (hbbft broadcast.rs [EXT]) -> rse ReedSolomon::new:
+ * validates the shard counts and writes the (data+parity) x data coding matrix
+ * M = V * inv(V[0..data]) (row-major) when out != NULL. */
+int hbg_coding_matrix(uint32_t data, uint32_t parity, uint8_t *out);
+
+/* Coding::encode(&mut [&mut [u8]]) -> rse encode: parity rows of every
+ * instance are (re)computed in place from the data rows. */
+int hbg_rs_encode(hbg_ctx *ctx, uint32_t data, uint32_t parity, uint64_t shard_len,
+                  uint8_t *shards, uint64_t shard_stride, uint64_t n, uint32_t flags);
+
+/* Coding::reconstruct_shards(&mut [Option<Box<[u8]>>]) -> rse reconstruct:
+ * present[k*N+i] != 0 marks shard i of instance k as present; missing rows are
+ * rebuilt in place from the FIRST `data` present rows (index order), present
+ * rows are left as received.  status[k] = 0 or a (negative) HBG_E_* code,
+ * e.g. HBG_E_TOO_FEW_SHARDS_PRESENT. */
+int hbg_rs_reconstruct(hbg_ctx *ctx, uint32_t data, uint32_t parity, uint64_t shard_len,
+                       uint8_t *shards, uint64_t shard_stride, const uint8_t *present,
+                       int32_t *status, uint64_t n, uint32_t flags);
+
+/* MerkleTree::from_vec(shards) (+ root_hash): SHA3-256 leaves, pair hashes,
+ * odd-node promotion.  levels: [n][hbg_merkle_nodes(N)][32]. */
+int hbg_merkle_build(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, const uint8_t *shards,
+                     uint64_t shard_stride, uint8_t *levels, uint64_t n, uint32_t flags);
+
+/* Proof::validate(n) for n_proofs proofs of one tree size N.
+ * values: [n_proofs] rows of value_len bytes at value_stride;
+ * digests: [n_proofs][hbg_merkle_depth(N)][32], ndigests[k] of them used;
+ * roots: [n_proofs][32];  ok[k] = 1 valid / 0 invalid. */
+int hbg_merkle_validate(hbg_ctx *ctx, uint32_t N, uint64_t value_len, const uint8_t *values,
+                        uint64_t value_stride, const uint32_t *index, const uint8_t *digests,
+                        const uint32_t *ndigests, const uint8_t *roots, uint8_t *ok,
+                        uint64_t n_proofs, uint32_t flags);
+
+/* Broadcast::send_shards fused (a2+a3+a4): payload k (payload_len[k] bytes at
+ * payloads + k*payload_stride) -> BE u32 length prefix, zero pad, chunk into N
+ * shards of shard_len, RS-encode, Merkle-tree.  Every payload_len[k] must give
+ * hbg_shard_len(N, payload_len[k]) == shard_len (else HBG_E_ARG).  Device mode
+ * additionally needs payload_stride % 4 == 0. */
+int hbg_rbc_encode_merkle(hbg_ctx *ctx, uint32_t N, const uint8_t *payloads,
+                          uint64_t payload_stride, const uint64_t *payload_len,
+                          uint64_t shard_len, uint8_t *shards, uint64_t shard_stride,
+                          uint8_t *levels, uint64_t n, uint32_t flags);
+
+/* decode_from_shards + glue_shards (a7+a8): reconstruct in place, rebuild the
+ * tree over all N shards, compare with roots[k]; on match glue the first
+ * data shards: payload_out + k*payload_stride gets payload_len[k] bytes and
+ * status[k] = HBG_DECODE_OK, else status[k] = HBG_DECODE_NONE. */
+int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards,
+                   uint64_t shard_stride, const uint8_t *present, const uint8_t *roots,
+                   uint8_t *payload_out, uint64_t payload_stride, uint64_t *payload_len,
+                   uint8_t *status, uint64_t n, uint32_t flags);
+
+/* Device-side seeded generator: row k of out gets nbytes of
+ * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */
+int hbg_synth_bytes(hbg_ctx *ctx, uint32_t tag, uint64_t first_instance, uint64_t nbytes,
+                    uint8_t *out, uint64_t out_stride, uint64_t n, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBGPU_H */

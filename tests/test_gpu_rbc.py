@@ -1,0 +1,311 @@
+"""GPU parity tests for the RBC coding path (family 1 + 2), through the C ABI.
+
+Every result is compared bit-for-bit with the oracle (oracle/: numpy + C
+restatements of rse / hbbft / tiny-keccak, pinned in tests/test_oracle_rbc.py)
+on the same seeded inputs.  Full BASELINE sizes (N=64, 1 MiB) are covered by
+size-independent properties: encode -> erase 2f -> decode round trips, proof
+validation of every leaf, and oracle spot checks of whole instances.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import corc, gf256, merkle, rbc as orbc, synth
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [1, 2, 3, 4, 5, 7, 10, 16, 31, 64, 100, 128, 256]
+
+
+def _bc():
+    from hydrabadger_amd import broadcast as bc
+    return bc
+
+
+@pytest.mark.parametrize("N", CONFIGS)
+@pytest.mark.parametrize("P", [0, 1, 5, 117, 1000, 4099])
+def test_send_shards_matches_oracle(N, P):
+    bc = _bc()
+    payload = synth.payload(N * 1000 + P, P)
+    shards, tree = bc.send_shards(payload, N)
+    ref_shards, ref_tree = orbc.send_shards(payload, N)
+    assert np.array_equal(shards, ref_shards)
+    assert tree.root_hash() == ref_tree.root_hash
+    assert [list(l) for l in tree.levels()] == [list(l) for l in ref_tree.levels]
+    for i in range(N):
+        p, rp = tree.proof(i), ref_tree.proof(i)
+        assert p.digests == rp.digests and p.index == rp.index and p.value == rp.value
+
+
+@pytest.mark.parametrize("D,Q", [(2, 2), (6, 10), (22, 42), (44, 84), (5, 5), (1, 1), (3, 7), (10, 3),
+                                 (100, 100), (17, 80), (200, 56), (1, 255), (255, 1)])
+@pytest.mark.parametrize("L", [1, 3, 4, 17, 136, 1001])
+def test_rs_encode_matches_oracle(D, Q, L):
+    bc = _bc()
+    n = 3
+    rows = np.frombuffer(synth.synth_bytes(synth.TAG_PAYLOAD, D * 7919 + Q * 31 + L, n * (D + Q) * L),
+                         np.uint8).reshape(n, D + Q, L).copy()
+    ref = rows.copy()
+    for k in range(n):
+        corc.rs_encode(D, Q, ref[k])
+    got = rows.copy()
+    bc.Coding(D, Q).encode_batch(got)
+    assert np.array_equal(got[:, :D], rows[:, :D])  # data untouched
+    assert np.array_equal(got, ref)
+
+
+def test_backblaze_kat_on_gpu():
+    bc = _bc()
+    sh = np.zeros((10, 2), np.uint8)
+    sh[:5] = [[0, 1], [4, 5], [2, 3], [6, 7], [8, 9]]
+    bc.Coding(5, 5).encode(sh)
+    assert sh[5:].tolist() == [[12, 13], [10, 11], [14, 15], [90, 91], [94, 95]]
+
+
+def test_encode_list_of_rows_and_errors():
+    bc = _bc()
+    rows = [bytearray(b"\x00\x01"), bytearray(b"\x04\x05"), bytearray(2), bytearray(2)]
+    bc.Coding(2, 2).encode(rows)
+    ref = np.zeros((4, 2), np.uint8)
+    ref[0], ref[1] = [0, 1], [4, 5]
+    corc.rs_encode(2, 2, ref)
+    assert [bytes(r) for r in rows] == [r.tobytes() for r in ref]
+    with pytest.raises(bc.RseError) as e:
+        bc.Coding(2, 2).encode([bytearray(2)] * 3)
+    assert e.value.kind == "TooFewShards"
+    with pytest.raises(bc.RseError) as e:
+        bc.Coding(2, 2).encode([bytearray(2), bytearray(3), bytearray(2), bytearray(2)])
+    assert e.value.kind == "IncorrectShardSize"
+    with pytest.raises(bc.RseError) as e:
+        bc.Coding(0, 2)
+    assert e.value.kind == "TooFewDataShards"
+    with pytest.raises(bc.RseError) as e:
+        bc.Coding(200, 57)
+    assert e.value.kind == "TooManyShards"
+
+
+@pytest.mark.parametrize("D,Q", [(2, 2), (6, 10), (22, 42), (44, 84), (1, 1), (3, 7), (86, 170), (255, 1)])
+def test_reconstruct_matches_oracle(D, Q):
+    bc = _bc()
+    N, L, n = D + Q, 257, 6
+    data = np.frombuffer(synth.synth_bytes(synth.TAG_PAYLOAD, N * 13 + 1, n * N * L), np.uint8).reshape(n, N, L).copy()
+    for k in range(n):
+        corc.rs_encode(D, Q, data[k])
+    present = np.ones((n, N), np.uint8)
+    for k in range(n):
+        erase = [0, Q, Q // 2, 1, max(Q - 1, 0), Q + 1][k]  # incl. all-present and too-few
+        m = synth.erasure_mask(1000 * D + k, N, min(erase, N))
+        present[k] = np.array(m, np.uint8)
+    damaged = data.copy()
+    damaged[present == 0] = 0xEE  # garbage where shards are absent
+    st = bc.Coding(D, Q).reconstruct_batch(damaged, present)
+    for k in range(n):
+        np_ = int(present[k].sum())
+        if np_ < D:
+            assert st[k] == -14  # TooFewShardsPresent
+            continue
+        assert st[k] == 0
+        ref = data[k].copy()
+        ref[present[k] == 0] = 0
+        assert corc.rs_reconstruct(D, Q, ref, present[k]) == 0
+        assert np.array_equal(damaged[k], ref), (k, D, Q)
+        assert np.array_equal(damaged[k], data[k])
+
+
+def test_reconstruct_keeps_present_as_received():
+    """rse uses the FIRST D present rows; a corrupted later present shard is
+    kept verbatim and does not influence the rebuilt rows."""
+    bc = _bc()
+    D, Q, L = 6, 10, 40
+    N = D + Q
+    sh = np.frombuffer(synth.synth_bytes(1, 99, N * L), np.uint8).reshape(N, L).copy()
+    corc.rs_encode(D, Q, sh)
+    present = np.ones(N, bool)
+    present[[0, 3, 7]] = False
+    rows = [sh[i].copy() if present[i] else None for i in range(N)]
+    rows[15] = rows[15].copy()
+    rows[15][0] ^= 0xFF  # corrupted, but not among the first D present
+    oracle_rows = [r.copy() if r is not None else None for r in rows]
+    gf256.ReedSolomon(D, Q).reconstruct(oracle_rows)
+    bc.Coding(D, Q).reconstruct_shards(rows)
+    for i in range(N):
+        assert np.array_equal(rows[i], oracle_rows[i]), i
+    assert rows[15][0] == sh[15][0] ^ 0xFF
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 7, 16, 64, 100, 128, 256])
+@pytest.mark.parametrize("L", [0, 1, 8, 135, 136, 137, 272, 1000])
+def test_merkle_build_matches_oracle(N, L):
+    bc = _bc()
+    vals = [synth.synth_bytes(1, N * 1000 + L * 7 + i, L) for i in range(N)]
+    t = bc.MerkleTree.from_vec(vals)
+    r = merkle.MerkleTree.from_vec(vals)
+    assert t.root_hash() == r.root_hash
+    assert t.levels() == r.levels
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 7, 16, 64, 100, 256])
+def test_proof_validate_matches_oracle(N):
+    bc = _bc()
+    L = 150
+    vals = [synth.synth_bytes(1, N * 31 + i, L) for i in range(N)]
+    r = merkle.MerkleTree.from_vec(vals)
+    proofs = []
+    for i in range(N):
+        p = r.proof(i)
+        proofs.append(bc.Proof(p.value, p.index, list(p.digests), p.root_hash))
+    # negatives: flipped value byte, wrong index, missing / extra digest, wrong root
+    bad = []
+    for i in range(min(N, 4)):
+        p = r.proof(i)
+        v = bytearray(p.value)
+        v[i % L] ^= 1
+        bad.append(bc.Proof(bytes(v), p.index, list(p.digests), p.root_hash))
+        bad.append(bc.Proof(p.value, (p.index + 1) % N, list(p.digests), p.root_hash))
+        bad.append(bc.Proof(p.value, p.index, list(p.digests)[:-1], p.root_hash))
+        bad.append(bc.Proof(p.value, p.index, list(p.digests) + [b"\x00" * 32], p.root_hash))
+        bad.append(bc.Proof(p.value, p.index, list(p.digests), b"\x01" * 32))
+    allp = proofs + bad
+    ok = bc.validate_proofs(allp, N)
+    ref = [merkle.Proof(p.value, p.index, list(p.digests), p.root_hash).validate(N) for p in allp]
+    assert ok.tolist() == [int(x) for x in ref]
+    assert all(ok[:N])
+
+
+@pytest.mark.parametrize("N", [1, 3, 4, 16, 64, 128])
+def test_decode_from_shards_matches_oracle(N):
+    bc = _bc()
+    data, parity = bc.shard_counts(N)
+    for trial, P in enumerate([0, 3, 100, 5000]):
+        payload = synth.payload(N * 10 + trial, P)
+        shards, tree = bc.send_shards(payload, N)
+        mask = synth.erasure_mask(N * 10 + trial, N, parity)
+        leaves = [shards[i].copy() if mask[i] else None for i in range(N)]
+        ref_leaves = [l.copy() if l is not None else None for l in leaves]
+        out = bc.decode_from_shards(leaves, bc.Coding(data, parity), data, tree.root_hash())
+        ref = orbc.decode_from_shards(ref_leaves, N, tree.root_hash())
+        assert out == ref == payload
+        # too few shards -> None
+        if parity:
+            m2 = synth.erasure_mask(N * 10 + trial + 1, N, parity + 1)
+            l2 = [shards[i].copy() if m2[i] else None for i in range(N)]
+            assert bc.decode_from_shards(l2, bc.Coding(data, parity), data, tree.root_hash()) is None
+        # wrong root -> None (faulty proposer)
+        l3 = [shards[i].copy() if mask[i] else None for i in range(N)]
+        assert bc.decode_from_shards(l3, bc.Coding(data, parity), data, b"\x42" * 32) is None
+
+
+def test_decode_corrupted_present_shard_is_none():
+    bc = _bc()
+    N = 16
+    data, parity = bc.shard_counts(N)
+    payload = synth.payload(5, 3000)
+    shards, tree = bc.send_shards(payload, N)
+    leaves = [shards[i].copy() for i in range(N)]
+    leaves[2] = None
+    leaves[9][7] ^= 0x10  # corrupt a used shard -> rebuilt tree root differs
+    ref = orbc.decode_from_shards([l.copy() if l is not None else None for l in leaves], N, tree.root_hash())
+    out = bc.decode_from_shards(leaves, bc.Coding(data, parity), data, tree.root_hash())
+    assert out is None and ref is None
+
+
+def test_decode_length_prefix_truncation():
+    """glue_shards takes `len` bytes and silently truncates when the value is
+    shorter; a forged length prefix with a matching root must behave the same."""
+    bc = _bc()
+    N = 4
+    data, parity = bc.shard_counts(N)
+    L = 10
+    sh = np.zeros((N, L), np.uint8)
+    sh[:data] = np.frombuffer(synth.synth_bytes(1, 3, data * L), np.uint8).reshape(data, L)
+    sh[0, :4] = [0, 0, 1, 0]  # claims 256 bytes, only 16 available
+    corc.rs_encode(data, parity, sh)
+    root = merkle.MerkleTree.from_vec([bytes(r) for r in sh]).root_hash
+    leaves = [sh[i].copy() for i in range(N)]
+    leaves[1] = None
+    out = bc.decode_from_shards(leaves, bc.Coding(data, parity), data, root)
+    ref = orbc.decode_from_shards([sh[i].copy() if i != 1 else None for i in range(N)], N, root)
+    assert out == ref and len(out) == data * L - 4
+
+
+# ------------------------------------------------------------------ device-resident batches (BASELINE sizes)
+def _torch():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _device_batch(N, P, n, first=0):
+    torch = _torch()
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    L = _lib.shard_len(N, P)
+    S = (L + 15) // 16 * 16
+    PS = (P + 15) // 16 * 16
+    dev = torch.device("cuda:0")
+    pay = torch.empty((n, PS), dtype=torch.uint8, device=dev)
+    bc.synth_bytes(synth.TAG_PAYLOAD, first, P, pay, device=True)
+    plen = torch.full((n,), P, dtype=torch.int64, device=dev)
+    shards = torch.empty((n, N, S), dtype=torch.uint8, device=dev)
+    levels = torch.empty((n, _lib.merkle_nodes(N), 32), dtype=torch.uint8, device=dev)
+    bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels, device=True)
+    torch.cuda.synchronize()
+    return pay, shards, levels, L, S
+
+
+def test_device_synth_matches_oracle():
+    torch = _torch()
+    bc = _bc()
+    out = torch.zeros((3, 64), dtype=torch.uint8, device="cuda:0")
+    bc.synth_bytes(1, 40, 61, out, device=True)
+    got = out.cpu().numpy()
+    for k in range(3):
+        assert got[k, :61].tobytes() == synth.synth_bytes(1, 40 + k, 61)
+
+
+@pytest.mark.parametrize("N,P,n", [(16, 65536, 24), (64, 1 << 20, 6), (128, 1 << 20, 3), (4, 230, 100)])
+def test_device_batch_encode_matches_oracle(N, P, n):
+    pay, shards, levels, L, S = _device_batch(N, P, n, first=11)
+    sh = shards.cpu().numpy()
+    lv = levels.cpu().numpy()
+    for k in [0, n // 2, n - 1]:
+        payload = np.frombuffer(synth.payload(11 + k, P), np.uint8).copy()
+        rs, rl = corc.rbc_encode_merkle(N, payload)
+        assert np.array_equal(sh[k, :, :L], rs), k
+        assert np.array_equal(lv[k], rl), k
+
+
+@pytest.mark.parametrize("N,P,n", [(64, 1 << 20, 8), (16, 65536, 32)])
+def test_device_roundtrip_erase_decode(N, P, n):
+    """Size-independent property at BASELINE sizes: encode -> erase exactly 2f
+    shards (seeded Fisher-Yates) -> decode == payload, every instance."""
+    torch = _torch()
+    bc = _bc()
+    pay, shards, levels, L, S = _device_batch(N, P, n, first=500)
+    data, parity = bc.shard_counts(N)
+    nodes = levels.shape[1]
+    present = torch.tensor([synth.erasure_mask(500 + k, N, parity) for k in range(n)], dtype=torch.uint8,
+                           device="cuda:0")
+    dmg = shards.clone()
+    dmg[present == 0] = 0x5A
+    roots = levels[:, nodes - 1, :].contiguous()
+    OS = (data * L + 15) // 16 * 16
+    out = torch.zeros((n, OS), dtype=torch.uint8, device="cuda:0")
+    plen = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    bc.rbc_decode_batch(N, L, dmg, present, roots, out, plen, st, device=True)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [1] * n
+    assert plen.cpu().tolist() == [P] * n
+    assert torch.equal(out[:, :P], pay[:, :P])
+    assert torch.equal(dmg[:, :, :L], shards[:, :, :L])
+    # flip the expected root of one instance -> None for that one only
+    roots2 = roots.clone()
+    roots2[1, 0] ^= 1
+    dmg2 = shards.clone()
+    bc.rbc_decode_batch(N, L, dmg2, present, roots2, out, plen, st, device=True)
+    torch.cuda.synchronize()
+    s = st.cpu().tolist()
+    assert s[1] == 0 and all(v == 1 for i, v in enumerate(s) if i != 1)
