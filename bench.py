@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--instances", type=int, default=2048, help="1 MiB proposals per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=512, help="instances in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=1024, help="instances in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     return ap.parse_args()
@@ -114,7 +114,8 @@ def main():
     from hydrabadger_amd import broadcast as bc
 
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # one dedicated stream: events and engine launches share it
+    torch.cuda.set_stream(stream)
     ctx = _lib.Context(local)
     ctx.set_stream(stream.cuda_stream)
 
@@ -178,9 +179,9 @@ def main():
     # ---- decode path: reconstruct exactly 2f erasures + tree + glue ----
     decode = None
     if not a.no_decode:
-        from oracle import synth  # seeded erasure masks only (inputs, not the checker)
+        from hydrabadger_amd import workload
         nd = min(B, 512)
-        present = torch.tensor([synth.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
+        present = torch.tensor([workload.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
                                dtype=torch.uint8, device=dev)
         roots = levels[:nd, nodes - 1, :].contiguous()
         OS = (data * L + 15) // 16 * 16

@@ -43,6 +43,7 @@ SIGNATURES = {
     "hbg_init": (_i, [C.POINTER(C.c_void_p), _i]),
     "hbg_free": (None, [_vp]),
     "hbg_set_stream": (_i, [_vp, _vp]),
+    "hbg_reset_stream": (_i, [_vp]),
     "hbg_sync": (_i, [_vp]),
     "hbg_strerror": (C.c_char_p, [_i]),
     "hbg_version": (C.c_char_p, []),
@@ -121,7 +122,11 @@ class Context:
             pass
 
     def set_stream(self, stream_handle: int | None) -> None:
-        check(lib().hbg_set_stream(self.h, stream_handle), "hbg_set_stream")
+        """Use a hipStream_t verbatim (0 / None = the HIP null stream)."""
+        check(lib().hbg_set_stream(self.h, stream_handle or None), "hbg_set_stream")
+
+    def reset_stream(self) -> None:
+        check(lib().hbg_reset_stream(self.h), "hbg_reset_stream")
 
     def sync(self) -> None:
         check(lib().hbg_sync(self.h), "hbg_sync")

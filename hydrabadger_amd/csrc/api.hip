@@ -251,7 +251,14 @@ void hbg_free(hbg_ctx* c) {
 int hbg_set_stream(hbg_ctx* c, void* s) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    c->stream = s ? (hipStream_t)s : c->own;
+    c->stream = (hipStream_t)s;
+    return HBG_OK;
+}
+
+int hbg_reset_stream(hbg_ctx* c) {
+    if (!c) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->stream = c->own;
     return HBG_OK;
 }
 

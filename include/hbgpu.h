@@ -68,9 +68,12 @@ typedef struct hbg_ctx hbg_ctx;
 /* ---- context ---- */
 int hbg_init(hbg_ctx **out, int device); /* device < 0: the current HIP device */
 void hbg_free(hbg_ctx *ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Enqueue on an external hipStream_t from now on (e.g.
+ * torch.cuda.current_stream().cuda_stream); the handle is used verbatim, so
+ * NULL selects the HIP null stream.  hbg_reset_stream() returns to the
+ * context's own non-blocking stream. */
 int hbg_set_stream(hbg_ctx *ctx, void *hip_stream);
+int hbg_reset_stream(hbg_ctx *ctx);
 int hbg_sync(hbg_ctx *ctx);
 const char *hbg_strerror(int code);
 const char *hbg_version(void);

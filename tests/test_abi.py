@@ -83,3 +83,11 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(dp, f)).read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", src).replace("oracle/", ""), f
+
+
+def test_workload_generator_matches_oracle_statement():
+    from hydrabadger_amd import workload
+    from oracle import synth
+    for inst in [0, 1, 77, 2 ** 33]:
+        for n, e in [(64, 42), (16, 10), (4, 2), (128, 84)]:
+            assert workload.erasure_mask(inst, n, e) == synth.erasure_mask(inst, n, e)

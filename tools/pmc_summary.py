@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSV passes: per kernel, mean counter value per
+dispatch, plus derived VALU utilisation and corrected HBM bytes.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half
+of a wide coalesced read stream -> x2 for the read side; WRITE_SIZE (KiB) is
+exact for 16-B streaming stores.  SQ_* cycle counters are in quad-cycles.
+"""
+from __future__ import annotations
+
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name: str) -> str:
+    n = name.split("(")[0]
+    return n.replace("void ", "").replace("hbg::", "")
+
+
+def load(root: str):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r.get("Kernel_Name", "?"))
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if "Start_Timestamp" in r and r.get("Start_Timestamp"):
+                try:
+                    dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+                except ValueError:
+                    pass
+    return acc, dur
+
+
+def main():
+    root = sys.argv[1]
+    acc, dur = load(root)
+    out = {}
+    for k, cs in acc.items():
+        if not k.startswith(("merkle", "rs_", "rbc_", "synth", "tdec", "bls", "g1_", "g2_", "pair")):
+            continue
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = {"counters": m}
+        if "SQ_INSTS_VALU" in m and "SQ_WAVES" in m:
+            d["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / max(m["SQ_WAVES"], 1)
+        if "SQ_ACTIVE_INST_VALU" in m and "SQ_BUSY_CYCLES" in m:
+            d["valu_active_per_busy"] = m["SQ_ACTIVE_INST_VALU"] / max(m["SQ_BUSY_CYCLES"], 1)
+        if "FETCH_SIZE" in m:
+            d["hbm_read_bytes_corrected"] = m["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in m:
+            d["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+        out[k] = d
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
