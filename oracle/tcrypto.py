@@ -1,0 +1,162 @@
+"""threshold_crypto restatement (TEST INFRASTRUCTURE ONLY — see oracle/__init__.py).
+
+Restates threshold_crypto [EXT, 0.3/0.4-era, unpinned] as hbbft's
+ThresholdDecrypt uses it, reached from the
+reference at /root/reference/src/hydrabadger/state.rs:486-487:
+
+  Ciphertext(U: G1, V: bytes, W: G2); encrypt_with_rng; Ciphertext::verify;
+  SecretKeyShare::decrypt_share_no_verify; PublicKeyShare::verify_decryption_share;
+  PublicKeySet::decrypt -> interpolate(t, first t+1 shares) + xor_with_hash;
+  hash_g2 / hash_g1_g2 (ChaChaRng-seeded try-and-increment G2 sampling).
+
+``hash_g2`` is the version-dependent row: "parity unpinned" (DESIGN.md).
+Randomness (r, polynomial coefficients) is an explicit argument here: the
+reference draws it from an entropy-seeded StdRng (state.rs:480), so runs are
+not reproducible there anyway; our harness seeds it.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from . import bls12_381 as B
+from .chacha import ChaChaRng
+from .merkle import sha3
+
+FQ_SHAVE_MASK = 0xFFFFFFFFFFFFFFFF >> 3
+
+
+def _rand_fq(rng: ChaChaRng) -> int:
+    """ff_derive ``Rand for Fq``: six next_u64 limbs (LE), top limb masked by
+    3 shave bits, rejected unless < p, read as a MONTGOMERY representation."""
+    while True:
+        limbs = [rng.next_u64() for _ in range(6)]
+        limbs[5] &= FQ_SHAVE_MASK
+        repr_int = sum(l << (64 * i) for i, l in enumerate(limbs))
+        if repr_int < B.P:
+            return B.fq_from_mont_repr(repr_int)
+
+
+def _rand_g2(rng: ChaChaRng):
+    """pairing ``Rand for G2``: x = Fq2{c0, c1}, greatest = next_u32 & 1,
+    get_point_from_x, scale_by_cofactor, retry on failure / identity."""
+    while True:
+        x = (_rand_fq(rng), _rand_fq(rng))
+        greatest = (rng.next_u32() & 1) == 1
+        p = B.g2_get_point_from_x(x, greatest)
+        if p is not None:
+            q = B.g2_scale_by_cofactor(p)
+            if q is not None:
+                return q
+
+
+def hash_g2(msg: bytes):
+    return _rand_g2(ChaChaRng(sha3(msg)))
+
+
+def hash_g1_g2(g1, msg: bytes):
+    m = sha3(msg) if len(msg) > 64 else bytes(msg)
+    return hash_g2(m + B.g1_compress(g1))
+
+
+def xor_with_hash(g1, data: bytes) -> bytes:
+    rng = ChaChaRng(sha3(B.g1_compress(g1)))
+    return bytes(b ^ (rng.next_u32() & 0xFF) for b in data)
+
+
+@dataclass
+class Ciphertext:
+    U: tuple
+    V: bytes
+    W: tuple
+
+    def verify(self) -> bool:
+        h = hash_g1_g2(self.U, self.V)
+        return B.pairing_check([(B.G1, self.W), (B.g1_neg(self.U), h)])
+
+
+def encrypt(pk, msg: bytes, r: int) -> Ciphertext:
+    """PublicKey::encrypt_with_rng with the scalar r given explicitly."""
+    u = B.g1_mul(B.G1, r)
+    v = xor_with_hash(B.g1_mul(pk, r), msg)
+    w = B.g2_mul(hash_g1_g2(u, v), r)
+    return Ciphertext(u, v, w)
+
+
+def decrypt_share(sk_share: int, ct: Ciphertext):
+    """SecretKeyShare::decrypt_share_no_verify: U * sk_i."""
+    return B.g1_mul(ct.U, sk_share)
+
+
+def verify_decryption_share(pk_share, share, ct: Ciphertext, h=None) -> bool:
+    """PublicKeyShare::verify_decryption_share: e(share, H) == e(pk_i, W)."""
+    h = hash_g1_g2(ct.U, ct.V) if h is None else h
+    return B.pairing_check([(share, h), (B.g1_neg(pk_share), ct.W)])
+
+
+class NotEnoughShares(Exception):
+    pass
+
+
+class DuplicateEntry(Exception):
+    pass
+
+
+def interpolate(t: int, items: list):
+    """threshold_crypto ``interpolate``: first t+1 (index, G1) items, x = index+1,
+    value at 0 of the Lagrange polynomial through them."""
+    samples = [(i + 1, s) for i, s in items[: t + 1]]
+    if len(samples) <= t:
+        raise NotEnoughShares()
+    xs = [x for x, _ in samples]
+    if len(set(xs)) != len(xs):
+        raise DuplicateEntry()
+    if t == 0:
+        return samples[0][1]
+    acc = None
+    for x, s in samples:
+        num, den = 1, 1
+        for x0 in xs:
+            if x0 != x:
+                num = num * x0 % B.R
+                den = den * (x0 - x) % B.R
+        lam = num * pow(den, -1, B.R) % B.R
+        acc = B.g1_add(acc, B.g1_mul(s, lam))
+    return acc
+
+
+def decrypt(t: int, shares: list, ct: Ciphertext) -> bytes:
+    """PublicKeySet::decrypt(shares, ct): shares = [(index, G1)] in iterator order."""
+    g = interpolate(t, shares)
+    return xor_with_hash(g, ct.V)
+
+
+class SecretKeySet:
+    """Polynomial of degree t over Fr with explicit coefficients."""
+
+    def __init__(self, coeffs: list):
+        self.coeffs = [c % B.R for c in coeffs]
+
+    @property
+    def threshold(self) -> int:
+        return len(self.coeffs) - 1
+
+    def secret_key_share(self, i: int) -> int:
+        x, acc = i + 1, 0
+        for c in reversed(self.coeffs):
+            acc = (acc * x + c) % B.R
+        return acc
+
+    def public_key(self):
+        return B.g1_mul(B.G1, self.coeffs[0])
+
+    def commitment(self) -> list:
+        return [B.g1_mul(B.G1, c) for c in self.coeffs]
+
+
+def public_key_share(commitment: list, i: int):
+    """PublicKeySet::public_key_share(i) = commitment evaluated at i+1."""
+    x = i + 1
+    acc = None
+    for c in reversed(commitment):
+        acc = B.g1_add(B.g1_mul(acc, x) if acc is not None else None, c)
+    return acc
