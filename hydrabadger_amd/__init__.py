@@ -7,6 +7,6 @@ The product is libhbgpu.so (C ABI: include/hbgpu.h; HIP kernels in csrc/).
 fallback: compute calls raise when the HIP library or a device is missing.
 Importing the package does not touch the GPU.
 """
-from . import _lib, broadcast  # noqa: F401
+from . import _lib, broadcast, threshold  # noqa: F401
 
-__all__ = ["_lib", "broadcast"]
+__all__ = ["_lib", "broadcast", "threshold"]

@@ -59,6 +59,10 @@ SIGNATURES = {
     "hbg_rbc_encode_merkle": (_i, [_vp, _u32, _u8p, _u64, _vp, _u64, _u8p, _u64, _u8p, _u64, _u32]),
     "hbg_rbc_decode": (_i, [_vp, _u32, _u64, _u8p, _u64, _u8p, _u8p, _u8p, _u64, _vp, _u8p, _u64, _u32]),
     "hbg_synth_bytes": (_i, [_vp, _u32, _u64, _u64, _u8p, _u64, _u64, _u32]),
+    "hbg_tdec_verify_shares": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
+    "hbg_ct_verify": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u32]),
+    "hbg_tdec_combine": (_i, [_vp, _u32, _u32, _u8p, _vp, _u8p, _vp, _u8p, _vp, _u32]),
+    "hbg_test_bls": (_i, [_vp, C.c_int, _u32, _vp, _u32, _vp, _u32]),
 }
 
 _lib = None

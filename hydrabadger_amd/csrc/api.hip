@@ -16,12 +16,14 @@
 #include "../../include/hbgpu.h"
 #include "gf256.h"
 #include "rbc_kernels.h"
+#include "tdec_kernels.h"
+#include "../../include/hbgpu_testing.h"
 
 using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 12;
+constexpr int kNumSlots = 16;
 
 struct Buf {
     void* p = nullptr;
@@ -492,6 +494,190 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
     HBG_TRY(hipMemcpyAsync(plen, dpl, 8 * n, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpy2DAsync(out, ostride, dout, OS, (uint64_t)D * L, n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+// ------------------------------------------------------------------ family 3
+namespace {
+
+struct CtTable {
+    uint32_t *ct_u, *coefH, *coefW;
+    int32_t* ct_status;
+};
+
+// Stage (host mode) and prepare a ciphertext table on the device.
+int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+             const uint8_t* W96, uint32_t flags, CtTable& t, const uint8_t** dV, const uint64_t** dVoff) {
+    const uint8_t *dU = U48, *dW = W96;
+    *dV = V;
+    *dVoff = V_off;
+    if (!(flags & HBG_DEVICE)) {
+        const uint64_t vlen = V_off[n_ct];
+        void *pu, *pw, *pv, *po;
+        HBG_CHECK(scratch(c, 0, 48ull * n_ct, &pu));
+        HBG_CHECK(scratch(c, 1, 96ull * n_ct, &pw));
+        HBG_CHECK(scratch(c, 2, vlen ? vlen : 1, &pv));
+        HBG_CHECK(scratch(c, 3, 8ull * (n_ct + 1), &po));
+        HBG_TRY(hipMemcpyAsync(pu, U48, 48ull * n_ct, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(pw, W96, 96ull * n_ct, hipMemcpyHostToDevice, c->stream));
+        if (vlen) HBG_TRY(hipMemcpyAsync(pv, V, vlen, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(po, V_off, 8ull * (n_ct + 1), hipMemcpyHostToDevice, c->stream));
+        dU = (const uint8_t*)pu;
+        dW = (const uint8_t*)pw;
+        *dV = (const uint8_t*)pv;
+        *dVoff = (const uint64_t*)po;
+    }
+    void *pcu, *pst, *ph, *pwc;
+    HBG_CHECK(scratch(c, 4, 4ull * bls::kAffWords * n_ct, &pcu));
+    HBG_CHECK(scratch(c, 5, 4ull * n_ct, &pst));
+    HBG_CHECK(scratch(c, 6, 4ull * bls::kLineWordsPerPoint * n_ct, &ph));
+    HBG_CHECK(scratch(c, 7, 4ull * bls::kLineWordsPerPoint * n_ct, &pwc));
+    t.ct_u = (uint32_t*)pcu;
+    t.ct_status = (int32_t*)pst;
+    t.coefH = (uint32_t*)ph;
+    t.coefW = (uint32_t*)pwc;
+    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW, c->stream));
+    return HBG_OK;
+}
+
+}  // namespace
+
+int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                           const uint8_t* W96, uint32_t n_pk, const uint8_t* pk48, uint64_t n, const uint8_t* share48,
+                           const uint32_t* share_ct, const uint32_t* share_pk, uint8_t* ok, uint32_t flags) {
+    if (!c || (n_ct && (!U48 || !V_off || !W96)) || (n_pk && !pk48) ||
+        (n && (!share48 || !share_ct || !share_pk || !ok)))
+        return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!(flags & HBG_DEVICE)) {
+        for (uint64_t k = 0; k < n; ++k)
+            if (share_ct[k] >= n_ct || share_pk[k] >= n_pk) return HBG_E_ARG;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    CtTable t;
+    const uint8_t* dV;
+    const uint64_t* dVoff;
+    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, t, &dV, &dVoff));
+    const uint8_t *dpk = pk48, *dsh = share48;
+    const uint32_t *dsc = share_ct, *dsp = share_pk;
+    uint8_t* dok = ok;
+    if (!(flags & HBG_DEVICE)) {
+        void *a, *b, *s1, *s2, *o;
+        HBG_CHECK(scratch(c, 8, 48ull * n_pk, &a));
+        HBG_CHECK(scratch(c, 9, 48ull * n, &b));
+        HBG_CHECK(scratch(c, 10, 8ull * n, &s1));
+        HBG_CHECK(scratch(c, 11, n, &o));
+        s2 = (uint8_t*)s1 + 4ull * n;
+        HBG_TRY(hipMemcpyAsync(a, pk48, 48ull * n_pk, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(b, share48, 48ull * n, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(s1, share_ct, 4ull * n, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(s2, share_pk, 4ull * n, hipMemcpyHostToDevice, c->stream));
+        dpk = (const uint8_t*)a;
+        dsh = (const uint8_t*)b;
+        dsc = (const uint32_t*)s1;
+        dsp = (const uint32_t*)s2;
+        dok = (uint8_t*)o;
+    }
+    void *paff, *pst;
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
+    HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
+    HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    HBG_TRY(bls::launch_tdec_verify_shares(n, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, (uint32_t*)paff,
+                                           (int32_t*)pst, dok, c->stream));
+    if (!(flags & HBG_DEVICE)) {
+        HBG_TRY(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, c->stream));
+        HBG_TRY(hipStreamSynchronize(c->stream));
+        return HBG_OK;
+    }
+    return finish(c, flags);
+}
+
+int hbg_ct_verify(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                  const uint8_t* W96, uint8_t* ok, uint32_t flags) {
+    if (!c || (n_ct && (!U48 || !V_off || !W96 || !ok))) return HBG_E_ARG;
+    if (n_ct == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    CtTable t;
+    const uint8_t* dV;
+    const uint64_t* dVoff;
+    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, t, &dV, &dVoff));
+    uint8_t* dok = ok;
+    if (!(flags & HBG_DEVICE)) {
+        void* o;
+        HBG_CHECK(scratch(c, 8, n_ct, &o));
+        dok = (uint8_t*)o;
+    }
+    HBG_TRY(bls::launch_tdec_ct_verify(n_ct, t.ct_u, t.ct_status, t.coefH, t.coefW, dok, c->stream));
+    if (!(flags & HBG_DEVICE)) {
+        HBG_TRY(hipMemcpyAsync(ok, dok, n_ct, hipMemcpyDeviceToHost, c->stream));
+        HBG_TRY(hipStreamSynchronize(c->stream));
+        return HBG_OK;
+    }
+    return finish(c, flags);
+}
+
+int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share48, const uint32_t* idx,
+                     const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status, uint32_t flags) {
+    if (!c || (n_ct && (!share48 || !idx || !V_off || !out || !status))) return HBG_E_ARG;
+    if (n_ct == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t m = (uint64_t)t + 1;
+    const uint8_t *dsh = share48, *dV = V;
+    const uint32_t* dix = idx;
+    const uint64_t* dVoff = V_off;
+    uint8_t* dout = out;
+    int32_t* dst = status;
+    uint64_t vlen = 0;
+    if (!(flags & HBG_DEVICE)) {
+        vlen = V_off[n_ct];
+        void *a, *b, *v, *o, *po, *s;
+        HBG_CHECK(scratch(c, 0, 48 * m * n_ct, &a));
+        HBG_CHECK(scratch(c, 1, 4 * m * n_ct, &b));
+        HBG_CHECK(scratch(c, 2, vlen ? vlen : 1, &v));
+        HBG_CHECK(scratch(c, 3, 8ull * (n_ct + 1), &po));
+        HBG_CHECK(scratch(c, 4, vlen ? vlen : 1, &o));
+        HBG_CHECK(scratch(c, 5, 4ull * n_ct, &s));
+        HBG_TRY(hipMemcpyAsync(a, share48, 48 * m * n_ct, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(b, idx, 4 * m * n_ct, hipMemcpyHostToDevice, c->stream));
+        if (vlen) HBG_TRY(hipMemcpyAsync(v, V, vlen, hipMemcpyHostToDevice, c->stream));
+        HBG_TRY(hipMemcpyAsync(po, V_off, 8ull * (n_ct + 1), hipMemcpyHostToDevice, c->stream));
+        dsh = (const uint8_t*)a;
+        dix = (const uint32_t*)b;
+        dV = (const uint8_t*)v;
+        dVoff = (const uint64_t*)po;
+        dout = (uint8_t*)o;
+        dst = (int32_t*)s;
+    }
+    void* scr;
+    HBG_CHECK(scratch(c, 6, 4ull * 32 * m * n_ct, &scr));
+    HBG_TRY(bls::launch_tdec_combine(n_ct, t, dsh, dix, dV, dVoff, dout, dst, (uint32_t*)scr, c->stream));
+    if (!(flags & HBG_DEVICE)) {
+        if (vlen) HBG_TRY(hipMemcpyAsync(out, dout, vlen, hipMemcpyDeviceToHost, c->stream));
+        HBG_TRY(hipMemcpyAsync(status, dst, 4ull * n_ct, hipMemcpyDeviceToHost, c->stream));
+        HBG_TRY(hipStreamSynchronize(c->stream));
+        return HBG_OK;
+    }
+    return finish(c, flags);
+}
+
+int hbg_test_bls(hbg_ctx* c, int op, uint32_t n, const uint32_t* in, uint32_t in_words, uint32_t* out,
+                 uint32_t out_words) {
+    if (!c || !in || !out || n == 0) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    void *di, *dout, *dl;
+    HBG_CHECK(scratch(c, 0, 4ull * in_words * n, &di));
+    HBG_CHECK(scratch(c, 1, 4ull * out_words * n, &dout));
+    HBG_CHECK(scratch(c, 2, 4ull * bls::kLineWordsPerPoint * n, &dl));
+    HBG_TRY(hipMemcpyAsync(di, in, 4ull * in_words * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemsetAsync(dout, 0, 4ull * out_words * n, c->stream));
+    HBG_TRY(bls::launch_tdec_test(op, n, (const uint32_t*)di, (uint32_t*)dout, in_words, out_words, (uint32_t*)dl,
+                                  c->stream));
+    HBG_TRY(hipMemcpyAsync(out, dout, 4ull * out_words * n, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipStreamSynchronize(c->stream));
     return HBG_OK;
 }

@@ -1,0 +1,845 @@
+// bls.h — BLS12-381 arithmetic for gfx950: one field element per work-item.
+//
+// Restates the zkcrypto `pairing` crate's bls12_381 module [EXT] as
+// threshold_crypto uses it.  Values are bit-identical
+// to the crate's (same Montgomery domain R = 2^384, same tower, same
+// G2Prepared line coefficients, same final-exponentiation chain), so every
+// intermediate can be unit-tested against oracle/bls12_381.py.
+//
+// gfx950 mapping
+//  * Fp = 12 x u32 limbs as an ext_vector so it travels in VGPRs across
+//    calls; fp_mul / fp_sqr are the only non-inlined primitives (one ~650-op
+//    body each: 288 v_mad_u64_u32 + 288 v_addc, see tools/gen_bls_fp.py),
+//    everything above them inlines, keeping code size bounded.
+//  * Fp2 / Fp6 / Fp12 are plain structs of Fp; exponentiations run rolled
+//    loops over constant exponent words (scalar loads, wave-uniform branches).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bls_consts.h"
+#include "bls_fp_mul.h"
+
+namespace hbg {
+namespace bls {
+
+typedef uint32_t Fp __attribute__((ext_vector_type(12)));
+
+#define BD __device__ __forceinline__
+
+template <int N>
+BD Fp fp_const(const uint32_t (&c)[N]) {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = c[i];
+    return r;
+}
+
+BD Fp fp_zero() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = 0u;
+    return r;
+}
+
+BD Fp fp_one() { return fp_const(kOne); }
+
+__device__ __noinline__ Fp fp_mul(Fp a, Fp b) {
+    uint32_t x[12], y[12], r[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        x[i] = a[i];
+        y[i] = b[i];
+    }
+    fp_mul_raw(r, x, y);
+    Fp o;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) o[i] = r[i];
+    return o;
+}
+
+__device__ __noinline__ Fp fp_sqr(Fp a) {
+    uint32_t x[12], r[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) x[i] = a[i];
+    fp_sqr_raw(r, x);
+    Fp o;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) o[i] = r[i];
+    return o;
+}
+
+BD Fp fp_add(const Fp& a, const Fp& b) {
+    Fp r, u;
+    uint32_t c = 0, br = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = __builtin_addc(a[i], b[i], c, &c);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) u[i] = __builtin_subc(r[i], kP[i], br, &br);
+    // a + b < 2p < 2^382: no carry out of limb 11; r >= p <=> no borrow
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = br ? r[i] : u[i];
+    return r;
+}
+
+BD Fp fp_sub(const Fp& a, const Fp& b) {
+    Fp r, u;
+    uint32_t br = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = __builtin_subc(a[i], b[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) u[i] = __builtin_addc(r[i], kP[i], c, &c);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = br ? u[i] : r[i];
+    return r;
+}
+
+BD bool fp_is_zero(const Fp& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) o |= a[i];
+    return o == 0;
+}
+
+BD bool fp_eq(const Fp& a, const Fp& b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) o |= a[i] ^ b[i];
+    return o == 0;
+}
+
+BD Fp fp_neg(const Fp& a) { return fp_sub(fp_zero(), a); }
+BD Fp fp_dbl(const Fp& a) { return fp_add(a, a); }
+
+BD Fp fp_select(bool c, const Fp& a, const Fp& b) {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = c ? a[i] : b[i];
+    return r;
+}
+
+// Montgomery <-> canonical
+BD Fp fp_to_mont(const Fp& raw) { return fp_mul(raw, fp_const(kR2)); }
+BD Fp fp_from_mont(const Fp& a) {
+    Fp one = fp_zero();
+    one[0] = 1u;
+    return fp_mul(a, one);
+}
+
+// canonical a > canonical b (both Montgomery)
+BD bool fp_gt(const Fp& a, const Fp& b) {
+    const Fp x = fp_from_mont(a), y = fp_from_mont(b);
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) (void)__builtin_subc(y[i], x[i], br, &br);
+    return br != 0;  // y - x borrows <=> x > y
+}
+
+// raw (canonical) limbs < p ?
+BD bool fp_raw_lt_p(const Fp& a) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) (void)__builtin_subc(a[i], kP[i], br, &br);
+    return br != 0;
+}
+
+// a^e for an exponent held in constant memory (nbits significant bits).
+__device__ __noinline__ Fp fp_pow(Fp a, const uint32_t* __restrict__ e, int nbits) {
+    Fp r = a;
+    for (int i = nbits - 2; i >= 0; --i) {
+        r = fp_sqr(r);
+        if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+    }
+    return r;
+}
+
+__device__ __constant__ static const uint32_t gExpPm2[12] = {
+    kExpPm2[0], kExpPm2[1], kExpPm2[2], kExpPm2[3], kExpPm2[4],  kExpPm2[5],
+    kExpPm2[6], kExpPm2[7], kExpPm2[8], kExpPm2[9], kExpPm2[10], kExpPm2[11]};
+__device__ __constant__ static const uint32_t gExpSqrt[12] = {
+    kExpSqrt[0], kExpSqrt[1], kExpSqrt[2], kExpSqrt[3], kExpSqrt[4],  kExpSqrt[5],
+    kExpSqrt[6], kExpSqrt[7], kExpSqrt[8], kExpSqrt[9], kExpSqrt[10], kExpSqrt[11]};
+__device__ __constant__ static const uint32_t gExpPm3d4[12] = {
+    kExpPm3d4[0], kExpPm3d4[1], kExpPm3d4[2], kExpPm3d4[3], kExpPm3d4[4],  kExpPm3d4[5],
+    kExpPm3d4[6], kExpPm3d4[7], kExpPm3d4[8], kExpPm3d4[9], kExpPm3d4[10], kExpPm3d4[11]};
+__device__ __constant__ static const uint32_t gExpPm1d2[12] = {
+    kExpPm1d2[0], kExpPm1d2[1], kExpPm1d2[2], kExpPm1d2[3], kExpPm1d2[4],  kExpPm1d2[5],
+    kExpPm1d2[6], kExpPm1d2[7], kExpPm1d2[8], kExpPm1d2[9], kExpPm1d2[10], kExpPm1d2[11]};
+
+constexpr int kPBits = 381;
+
+BD Fp fp_inv(const Fp& a) { return fp_pow(a, gExpPm2, kPBits); }
+
+// sqrt for p = 3 mod 4; ok = a is a square
+BD Fp fp_sqrt(const Fp& a, bool& ok) {
+    const Fp s = fp_pow(a, gExpSqrt, 379);  // (p+1)/4 has 379 bits
+    ok = fp_eq(fp_sqr(s), a);
+    return s;
+}
+
+// big-endian bytes <-> raw limbs
+BD Fp fp_from_be(const uint8_t* p) {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        const uint8_t* q = p + 44 - 4 * i;
+        r[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+    return r;
+}
+
+BD void fp_to_be(uint8_t* p, const Fp& raw) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        uint8_t* q = p + 44 - 4 * i;
+        q[0] = (uint8_t)(raw[i] >> 24);
+        q[1] = (uint8_t)(raw[i] >> 16);
+        q[2] = (uint8_t)(raw[i] >> 8);
+        q[3] = (uint8_t)raw[i];
+    }
+}
+
+// ============================================================== Fp2 = Fp[u]/(u^2+1)
+struct Fp2 {
+    Fp c0, c1;
+};
+
+BD Fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+BD Fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+BD Fp2 fp2_add(const Fp2& a, const Fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+BD Fp2 fp2_sub(const Fp2& a, const Fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+BD Fp2 fp2_neg(const Fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+BD Fp2 fp2_dbl(const Fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+BD Fp2 fp2_conj(const Fp2& a) { return {a.c0, fp_neg(a.c1)}; }
+BD bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BD bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BD Fp2 fp2_select(bool c, const Fp2& a, const Fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
+
+BD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
+    const Fp t0 = fp_mul(a.c0, b.c0);
+    const Fp t1 = fp_mul(a.c1, b.c1);
+    const Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+    return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+BD Fp2 fp2_sqr(const Fp2& a) {
+    const Fp t = fp_mul(a.c0, a.c1);
+    return {fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+}
+
+BD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return {fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+
+// * (1 + u)
+BD Fp2 fp2_mul_xi(const Fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+BD Fp2 fp2_mul_small(const Fp2& a, int k) {
+    Fp2 r = a;
+    for (int i = 1; i < k; ++i) r = fp2_add(r, a);
+    return r;
+}
+
+BD Fp2 fp2_inv(const Fp2& a) {
+    const Fp t = fp_inv(fp_add(fp_sqr(a.c0), fp_sqr(a.c1)));
+    return {fp_mul(a.c0, t), fp_neg(fp_mul(a.c1, t))};
+}
+
+// canonical lexicographic a > b (the crate's Fq2 Ord: c1 first, then c0)
+BD bool fp2_gt(const Fp2& a, const Fp2& b) {
+    if (!fp_eq(a.c1, b.c1)) return fp_gt(a.c1, b.c1);
+    return fp_gt(a.c0, b.c0);
+}
+
+__device__ __noinline__ void fp2_pow_inplace(Fp2* x, const uint32_t* __restrict__ e, int nbits) {
+    const Fp2 a = *x;
+    Fp2 r = a;
+    for (int i = nbits - 2; i >= 0; --i) {
+        r = fp2_sqr(r);
+        if ((e[i >> 5] >> (i & 31)) & 1u) r = fp2_mul(r, a);
+    }
+    *x = r;
+}
+
+// Algorithm 9 of eprint 2012/685 (the crate's Fq2::sqrt); ok = square.
+BD Fp2 fp2_sqrt(const Fp2& a, bool& ok) {
+    ok = true;
+    if (fp2_is_zero(a)) return a;
+    Fp2 a1 = a;
+    fp2_pow_inplace(&a1, gExpPm3d4, 379);
+    const Fp2 alpha = fp2_mul(fp2_sqr(a1), a);
+    const Fp2 a0 = fp2_mul(fp2_conj(alpha), alpha);
+    const Fp2 mone = fp2_neg(fp2_one());
+    if (fp2_eq(a0, mone)) {
+        ok = false;
+        return a;
+    }
+    a1 = fp2_mul(a1, a);
+    if (fp2_eq(alpha, mone)) return {fp_neg(a1.c1), a1.c0};  // a1 * u
+    Fp2 b = {fp_add(alpha.c0, fp_one()), alpha.c1};
+    fp2_pow_inplace(&b, gExpPm1d2, 380);
+    return fp2_mul(a1, b);
+}
+
+template <int N>
+BD Fp2 fp2_const(const uint32_t (&c)[N]) {
+    Fp2 r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        r.c0[i] = c[i];
+        r.c1[i] = c[12 + i];
+    }
+    return r;
+}
+
+// ============================================================== Fp6 = Fp2[v]/(v^3 - xi)
+struct Fp6 {
+    Fp2 c0, c1, c2;
+};
+
+BD Fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
+BD Fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+BD Fp6 fp6_add(const Fp6& a, const Fp6& b) { return {fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+BD Fp6 fp6_sub(const Fp6& a, const Fp6& b) { return {fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+BD Fp6 fp6_neg(const Fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+BD Fp6 fp6_mul_by_v(const Fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
+BD bool fp6_eq(const Fp6& a, const Fp6& b) { return fp2_eq(a.c0, b.c0) && fp2_eq(a.c1, b.c1) && fp2_eq(a.c2, b.c2); }
+
+BD Fp6 fp6_mul(const Fp6& a, const Fp6& b) {
+    const Fp2 t0 = fp2_mul(a.c0, b.c0), t1 = fp2_mul(a.c1, b.c1), t2 = fp2_mul(a.c2, b.c2);
+    Fp6 r;
+    r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
+    r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+    r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+    return r;
+}
+
+// a * (b0 + b1 v)   (the crate's Fq6::mul_by_01)
+BD Fp6 fp6_mul_by_01(const Fp6& a, const Fp2& b0, const Fp2& b1) {
+    const Fp2 t0 = fp2_mul(a.c0, b0), t1 = fp2_mul(a.c1, b1);
+    Fp6 r;
+    r.c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), b1), t1)), t0);
+    r.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+    r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), b0), t0), t1);
+    return r;
+}
+
+// a * (b1 v)   (the crate's Fq6::mul_by_1)
+BD Fp6 fp6_mul_by_1(const Fp6& a, const Fp2& b1) {
+    return {fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+// Non-inlined, pointer-passing forms of the heavy tower ops.  Operands travel
+// through private memory so each function is register-allocated on its own
+// (inlining the whole tower into one kernel needs ~460 live registers).
+__device__ __noinline__ void fp6_mul_p(Fp6* r, const Fp6* a, const Fp6* b) { *r = fp6_mul(*a, *b); }
+__device__ __noinline__ void fp6_mul_by_01_p(Fp6* r, const Fp6* a, const Fp2* b0, const Fp2* b1) {
+    *r = fp6_mul_by_01(*a, *b0, *b1);
+}
+__device__ __noinline__ void fp6_mul_by_1_p(Fp6* r, const Fp6* a, const Fp2* b1) { *r = fp6_mul_by_1(*a, *b1); }
+
+BD Fp6 fp6_inv(const Fp6& a) {
+    const Fp2 c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+    const Fp2 c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+    const Fp2 c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+    const Fp2 t = fp2_inv(fp2_add(fp2_mul(a.c0, c0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2)))));
+    return {fp2_mul(c0, t), fp2_mul(c1, t), fp2_mul(c2, t)};
+}
+
+template <int K>
+BD Fp6 fp6_frob(const Fp6& a) {
+    const Fp2 x0 = (K & 1) ? fp2_conj(a.c0) : a.c0;
+    const Fp2 x1 = (K & 1) ? fp2_conj(a.c1) : a.c1;
+    const Fp2 x2 = (K & 1) ? fp2_conj(a.c2) : a.c2;
+    if constexpr (K == 1) return {x0, fp2_mul(x1, fp2_const(kFrob6c1_1)), fp2_mul(x2, fp2_const(kFrob6c2_1))};
+    if constexpr (K == 2) return {x0, fp2_mul(x1, fp2_const(kFrob6c1_2)), fp2_mul(x2, fp2_const(kFrob6c2_2))};
+    if constexpr (K == 3) return {x0, fp2_mul(x1, fp2_const(kFrob6c1_3)), fp2_mul(x2, fp2_const(kFrob6c2_3))};
+    return a;
+}
+
+// ============================================================== Fp12 = Fp6[w]/(w^2 - v)
+struct Fp12 {
+    Fp6 c0, c1;
+};
+
+BD Fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+BD Fp12 fp12_conj(const Fp12& a) { return {a.c0, fp6_neg(a.c1)}; }
+BD bool fp12_eq(const Fp12& a, const Fp12& b) { return fp6_eq(a.c0, b.c0) && fp6_eq(a.c1, b.c1); }
+BD bool fp12_is_one(const Fp12& a) { return fp12_eq(a, fp12_one()); }
+
+__device__ __noinline__ void fp12_mul_p(Fp12* r, const Fp12* a, const Fp12* b) {
+    Fp6 t0, t1, t2, s0, s1;
+    fp6_mul_p(&t0, &a->c0, &b->c0);
+    fp6_mul_p(&t1, &a->c1, &b->c1);
+    s0 = fp6_add(a->c0, a->c1);
+    s1 = fp6_add(b->c0, b->c1);
+    fp6_mul_p(&t2, &s0, &s1);
+    r->c1 = fp6_sub(t2, fp6_add(t0, t1));
+    r->c0 = fp6_add(t0, fp6_mul_by_v(t1));
+}
+
+// the crate's Fq12::square (complex squaring, 2 Fq6 mults)
+__device__ __noinline__ void fp12_sqr_p(Fp12* r, const Fp12* a) {
+    Fp6 ab, c0, c0c1;
+    fp6_mul_p(&ab, &a->c0, &a->c1);
+    c0c1 = fp6_add(a->c0, a->c1);
+    c0 = fp6_add(fp6_mul_by_v(a->c1), a->c0);
+    fp6_mul_p(&c0, &c0, &c0c1);
+    c0 = fp6_sub(c0, ab);
+    r->c1 = fp6_add(ab, ab);
+    r->c0 = fp6_sub(c0, fp6_mul_by_v(ab));
+}
+
+__device__ __noinline__ void fp12_inv_p(Fp12* r, const Fp12* a) {
+    Fp6 t0, t1, t;
+    fp6_mul_p(&t0, &a->c0, &a->c0);
+    fp6_mul_p(&t1, &a->c1, &a->c1);
+    t = fp6_inv(fp6_sub(t0, fp6_mul_by_v(t1)));
+    Fp6 c0, c1;
+    fp6_mul_p(&c0, &a->c0, &t);
+    fp6_mul_p(&c1, &a->c1, &t);
+    r->c0 = c0;
+    r->c1 = fp6_neg(c1);
+}
+
+template <int K>
+__device__ __noinline__ void fp12_frob_p(Fp12* r, const Fp12* a) {
+    const Fp6 c0 = fp6_frob<K>(a->c0), c1 = fp6_frob<K>(a->c1);
+    Fp2 g;
+    if constexpr (K == 1) g = fp2_const(kFrob12c1_1);
+    if constexpr (K == 2) g = fp2_const(kFrob12c1_2);
+    if constexpr (K == 3) g = fp2_const(kFrob12c1_3);
+    r->c0 = c0;
+    r->c1 = {fp2_mul(c1.c0, g), fp2_mul(c1.c1, g), fp2_mul(c1.c2, g)};
+}
+
+// f * (c0 + c1 v + c4 v w)   (the crate's Fq12::mul_by_014)
+__device__ __noinline__ void fp12_mul_by_014_p(Fp12* f, const Fp2* c0, const Fp2* c1, const Fp2* c4) {
+    Fp6 aa, bb, t;
+    fp6_mul_by_01_p(&aa, &f->c0, c0, c1);
+    fp6_mul_by_1_p(&bb, &f->c1, c4);
+    const Fp2 o = fp2_add(*c1, *c4);
+    t = fp6_add(f->c1, f->c0);
+    fp6_mul_by_01_p(&t, &t, c0, &o);
+    f->c1 = fp6_sub(fp6_sub(t, aa), bb);
+    f->c0 = fp6_add(fp6_mul_by_v(bb), aa);
+}
+
+// Granger-Scott cyclotomic squaring (valid after the easy part of the final
+// exponentiation: same values as plain squaring there).
+BD void fp4_sqr(Fp2& r0, Fp2& r1, const Fp2& a, const Fp2& b) {
+    const Fp2 t0 = fp2_sqr(a), t1 = fp2_sqr(b);
+    r0 = fp2_add(fp2_mul_xi(t1), t0);
+    r1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+}
+
+BD Fp12 fp12_cyclotomic_sqr_v(const Fp12& f) {
+    // z0..z5 = c0.c0, c1.c1, c1.c0, c0.c2, c0.c1, c1.c2
+    Fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+    Fp2 t0, t1, t2, t3;
+    fp4_sqr(t0, t1, z0, z1);
+    z0 = fp2_add(fp2_dbl(fp2_sub(t0, z0)), t0);
+    z1 = fp2_add(fp2_dbl(fp2_add(t1, z1)), t1);
+    fp4_sqr(t0, t1, z2, z3);
+    fp4_sqr(t2, t3, z4, z5);
+    z4 = fp2_add(fp2_dbl(fp2_sub(t0, z4)), t0);
+    z5 = fp2_add(fp2_dbl(fp2_add(t1, z5)), t1);
+    t0 = fp2_mul_xi(t3);
+    z2 = fp2_add(fp2_dbl(fp2_add(t0, z2)), t0);
+    z3 = fp2_add(fp2_dbl(fp2_sub(t2, z3)), t2);
+    return {{z0, z4, z3}, {z2, z1, z5}};
+}
+
+__device__ __noinline__ void fp12_cyc_sqr_p(Fp12* r, const Fp12* f) { *r = fp12_cyclotomic_sqr_v(*f); }
+
+// *f = conj(f^e) for a 64-bit e with top set bit `top` (cyclotomic squarings);
+// with e = |x| this is the crate's exp_by_x (x < 0).
+__device__ __noinline__ void fp12_cyc_pow_conj(Fp12* f, uint64_t e, int top) {
+    Fp12 a = *f;
+    Fp12 r = a;
+    for (int i = top - 1; i >= 0; --i) {
+        fp12_cyc_sqr_p(&r, &r);
+        if ((e >> i) & 1ull) fp12_mul_p(&r, &r, &a);
+    }
+    *f = fp12_conj(r);
+}
+
+BD void fp12_exp_by_x_inplace(Fp12* f) { fp12_cyc_pow_conj(f, kBlsX, 63); }
+
+// ============================================================== curves
+struct G1 {  // Jacobian; infinity <=> Z == 0
+    Fp x, y, z;
+};
+struct G1A {
+    Fp x, y;
+    bool inf;
+};
+struct G2 {
+    Fp2 x, y, z;
+};
+struct G2A {
+    Fp2 x, y;
+    bool inf;
+};
+
+// ---- G1 (y^2 = x^3 + 4), dbl-2009-l / add-2007-bl (a = 0)
+BD G1 g1_dbl(const G1& p) {
+    const Fp A = fp_sqr(p.x), B = fp_sqr(p.y), C = fp_sqr(B);
+    const Fp D = fp_dbl(fp_sub(fp_sub(fp_sqr(fp_add(p.x, B)), A), C));
+    const Fp E = fp_add(fp_dbl(A), A);
+    const Fp F = fp_sqr(E);
+    G1 r;
+    r.x = fp_sub(F, fp_dbl(D));
+    r.y = fp_sub(fp_mul(E, fp_sub(D, r.x)), fp_dbl(fp_dbl(fp_dbl(C))));
+    r.z = fp_dbl(fp_mul(p.y, p.z));
+    return r;
+}
+
+// p + q with q affine (not infinity)
+BD G1 g1_add_mixed(const G1& p, const Fp& qx, const Fp& qy) {
+    if (fp_is_zero(p.z)) return {qx, qy, fp_one()};
+    const Fp Z1Z1 = fp_sqr(p.z);
+    const Fp U2 = fp_mul(qx, Z1Z1);
+    const Fp S2 = fp_mul(fp_mul(qy, p.z), Z1Z1);
+    const Fp H = fp_sub(U2, p.x);
+    const Fp rr = fp_dbl(fp_sub(S2, p.y));
+    if (fp_is_zero(H)) {
+        if (fp_is_zero(rr)) return g1_dbl(p);
+        return {fp_one(), fp_one(), fp_zero()};
+    }
+    const Fp HH = fp_sqr(H);
+    const Fp I = fp_dbl(fp_dbl(HH));
+    const Fp J = fp_mul(H, I);
+    const Fp V = fp_mul(p.x, I);
+    G1 r;
+    r.x = fp_sub(fp_sub(fp_sqr(rr), J), fp_dbl(V));
+    r.y = fp_sub(fp_mul(rr, fp_sub(V, r.x)), fp_dbl(fp_mul(p.y, J)));
+    r.z = fp_sub(fp_sub(fp_sqr(fp_add(p.z, H)), Z1Z1), HH);
+    return r;
+}
+
+BD G1 g1_add(const G1& p, const G1& q) {
+    if (fp_is_zero(p.z)) return q;
+    if (fp_is_zero(q.z)) return p;
+    const Fp Z1Z1 = fp_sqr(p.z), Z2Z2 = fp_sqr(q.z);
+    const Fp U1 = fp_mul(p.x, Z2Z2), U2 = fp_mul(q.x, Z1Z1);
+    const Fp S1 = fp_mul(fp_mul(p.y, q.z), Z2Z2), S2 = fp_mul(fp_mul(q.y, p.z), Z1Z1);
+    const Fp H = fp_sub(U2, U1);
+    const Fp rr = fp_dbl(fp_sub(S2, S1));
+    if (fp_is_zero(H)) {
+        if (fp_is_zero(rr)) return g1_dbl(p);
+        return {fp_one(), fp_one(), fp_zero()};
+    }
+    const Fp I = fp_sqr(fp_dbl(H));
+    const Fp J = fp_mul(H, I);
+    const Fp V = fp_mul(U1, I);
+    G1 r;
+    r.x = fp_sub(fp_sub(fp_sqr(rr), J), fp_dbl(V));
+    r.y = fp_sub(fp_mul(rr, fp_sub(V, r.x)), fp_dbl(fp_mul(S1, J)));
+    r.z = fp_mul(fp_sub(fp_sub(fp_sqr(fp_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+    return r;
+}
+
+BD G1A g1_to_affine(const G1& p) {
+    if (fp_is_zero(p.z)) return {fp_zero(), fp_zero(), true};
+    const Fp zi = fp_inv(p.z), zi2 = fp_sqr(zi);
+    return {fp_mul(p.x, zi2), fp_mul(p.y, fp_mul(zi2, zi)), false};
+}
+
+BD bool g1_on_curve(const Fp& x, const Fp& y) {
+    return fp_eq(fp_sqr(y), fp_add(fp_mul(fp_sqr(x), x), fp_const(kFour)));
+}
+
+// [k]P for a 64-bit scalar (left to right), P affine
+BD G1 g1_mul_u64(const Fp& px, const Fp& py, uint64_t k) {
+    G1 r = {fp_one(), fp_one(), fp_zero()};
+    for (int i = 63; i >= 0; --i) {
+        r = g1_dbl(r);
+        if ((k >> i) & 1ull) r = g1_add_mixed(r, px, py);
+    }
+    return r;
+}
+
+// P in G1  <=>  phi(P) == [-x^2] P,  phi(x, y) = (beta x, y)   (Bowe, eprint 2019/814)
+BD bool g1_in_subgroup(const Fp& px, const Fp& py) {
+    // [x^2]P = [|x|]([|x|]P);  [-x^2]P = -[x^2]P
+    G1 t = g1_mul_u64(px, py, kBlsX);
+    const G1A ta = g1_to_affine(t);
+    if (ta.inf) return false;
+    t = g1_mul_u64(ta.x, ta.y, kBlsX);
+    const G1A u = g1_to_affine(t);
+    if (u.inf) return false;
+    // compare (beta x, y) with (u.x, -u.y)
+    return fp_eq(fp_mul(px, fp_const(kBeta)), u.x) && fp_eq(py, fp_neg(u.y));
+}
+
+// zcash compressed G1 -> affine (Montgomery).  status: 0 ok, else invalid.
+BD bool g1_decompress(const uint8_t* b, G1A& out, bool check_subgroup) {
+    const uint8_t f = b[0];
+    out.inf = false;
+    if (!(f & 0x80)) return false;
+    if (f & 0x40) {  // infinity: everything else must be zero
+        bool z = (f & 0x3F) == 0;
+        for (int i = 1; i < 48; ++i) z &= b[i] == 0;
+        out.inf = true;
+        out.x = fp_zero();
+        out.y = fp_zero();
+        return z;
+    }
+    Fp raw = fp_from_be(b);
+    raw[11] &= 0x1FFFFFFFu;
+    if (!fp_raw_lt_p(raw)) return false;
+    const Fp x = fp_to_mont(raw);
+    bool ok;
+    Fp y = fp_sqrt(fp_add(fp_mul(fp_sqr(x), x), fp_const(kFour)), ok);
+    if (!ok) return false;
+    const Fp ny = fp_neg(y);
+    const bool want_greatest = (f & 0x20) != 0;
+    const bool y_greatest = fp_gt(y, ny);
+    out.x = x;
+    out.y = (y_greatest == want_greatest) ? y : ny;
+    if (check_subgroup && !g1_in_subgroup(out.x, out.y)) return false;
+    return true;
+}
+
+BD void g1_compress(uint8_t* b, const G1A& p) {
+    if (p.inf) {
+        b[0] = 0xC0;
+        for (int i = 1; i < 48; ++i) b[i] = 0;
+        return;
+    }
+    fp_to_be(b, fp_from_mont(p.x));
+    b[0] |= 0x80;
+    if (fp_gt(p.y, fp_neg(p.y))) b[0] |= 0x20;
+}
+
+// ---- G2 (y^2 = x^3 + 4(u+1)), Jacobian
+BD G2 g2_dbl_v(const G2& p) {
+    const Fp2 A = fp2_sqr(p.x), B = fp2_sqr(p.y), C = fp2_sqr(B);
+    const Fp2 D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(p.x, B)), A), C));
+    const Fp2 E = fp2_add(fp2_dbl(A), A);
+    const Fp2 F = fp2_sqr(E);
+    G2 r;
+    r.x = fp2_sub(F, fp2_dbl(D));
+    r.y = fp2_sub(fp2_mul(E, fp2_sub(D, r.x)), fp2_dbl(fp2_dbl(fp2_dbl(C))));
+    r.z = fp2_dbl(fp2_mul(p.y, p.z));
+    return r;
+}
+
+__device__ __noinline__ void g2_dbl_p(G2* r, const G2* p) { *r = g2_dbl_v(*p); }
+BD G2 g2_dbl(const G2& p) {
+    G2 r;
+    g2_dbl_p(&r, &p);
+    return r;
+}
+
+BD G2 g2_add_mixed_v(const G2& p, const Fp2& qx, const Fp2& qy) {
+    if (fp2_is_zero(p.z)) return {qx, qy, fp2_one()};
+    const Fp2 Z1Z1 = fp2_sqr(p.z);
+    const Fp2 U2 = fp2_mul(qx, Z1Z1);
+    const Fp2 S2 = fp2_mul(fp2_mul(qy, p.z), Z1Z1);
+    const Fp2 H = fp2_sub(U2, p.x);
+    const Fp2 rr = fp2_dbl(fp2_sub(S2, p.y));
+    if (fp2_is_zero(H)) {
+        if (fp2_is_zero(rr)) return g2_dbl(p);
+        return {fp2_one(), fp2_one(), fp2_zero()};
+    }
+    const Fp2 HH = fp2_sqr(H);
+    const Fp2 I = fp2_dbl(fp2_dbl(HH));
+    const Fp2 J = fp2_mul(H, I);
+    const Fp2 V = fp2_mul(p.x, I);
+    G2 r;
+    r.x = fp2_sub(fp2_sub(fp2_sqr(rr), J), fp2_dbl(V));
+    r.y = fp2_sub(fp2_mul(rr, fp2_sub(V, r.x)), fp2_dbl(fp2_mul(p.y, J)));
+    r.z = fp2_sub(fp2_sub(fp2_sqr(fp2_add(p.z, H)), Z1Z1), HH);
+    return r;
+}
+
+__device__ __noinline__ void g2_add_mixed_p(G2* r, const G2* p, const Fp2* qx, const Fp2* qy) {
+    *r = g2_add_mixed_v(*p, *qx, *qy);
+}
+BD G2 g2_add_mixed(const G2& p, const Fp2& qx, const Fp2& qy) {
+    G2 r;
+    g2_add_mixed_p(&r, &p, &qx, &qy);
+    return r;
+}
+
+BD G2A g2_to_affine(const G2& p) {
+    if (fp2_is_zero(p.z)) return {fp2_zero(), fp2_zero(), true};
+    const Fp2 zi = fp2_inv(p.z), zi2 = fp2_sqr(zi);
+    return {fp2_mul(p.x, zi2), fp2_mul(p.y, fp2_mul(zi2, zi)), false};
+}
+
+BD bool g2_on_curve(const Fp2& x, const Fp2& y) {
+    const Fp2 b = {fp_const(kB2), fp_const(kB2)};
+    return fp2_eq(fp2_sqr(y), fp2_add(fp2_mul(fp2_sqr(x), x), b));
+}
+
+BD G2 g2_mul_u64(const Fp2& px, const Fp2& py, uint64_t k) {
+    G2 r = {fp2_one(), fp2_one(), fp2_zero()};
+    for (int i = 63; i >= 0; --i) {
+        r = g2_dbl(r);
+        if ((k >> i) & 1ull) r = g2_add_mixed(r, px, py);
+    }
+    return r;
+}
+
+// Q in G2  <=>  psi(Q) == [x] Q   (Scott, eprint 2021/1130)
+BD bool g2_in_subgroup(const Fp2& qx, const Fp2& qy) {
+    const G2A t = g2_to_affine(g2_mul_u64(qx, qy, kBlsX));  // [|x|]Q
+    if (t.inf) return false;
+    const Fp2 psx = fp2_mul(fp2_conj(qx), fp2_const(kPsiX));
+    const Fp2 psy = fp2_mul(fp2_conj(qy), fp2_const(kPsiY));
+    return fp2_eq(psx, t.x) && fp2_eq(psy, fp2_neg(t.y));  // [x]Q = -[|x|]Q
+}
+
+BD bool g2_decompress(const uint8_t* b, G2A& out, bool check_subgroup) {
+    const uint8_t f = b[0];
+    out.inf = false;
+    if (!(f & 0x80)) return false;
+    if (f & 0x40) {
+        bool z = (f & 0x3F) == 0;
+        for (int i = 1; i < 96; ++i) z &= b[i] == 0;
+        out.inf = true;
+        out.x = fp2_zero();
+        out.y = fp2_zero();
+        return z;
+    }
+    Fp r1 = fp_from_be(b), r0 = fp_from_be(b + 48);
+    r1[11] &= 0x1FFFFFFFu;
+    if (!fp_raw_lt_p(r1) || !fp_raw_lt_p(r0)) return false;
+    const Fp2 x = {fp_to_mont(r0), fp_to_mont(r1)};
+    const Fp2 b2 = {fp_const(kB2), fp_const(kB2)};
+    bool ok;
+    const Fp2 y = fp2_sqrt(fp2_add(fp2_mul(fp2_sqr(x), x), b2), ok);
+    if (!ok) return false;
+    const Fp2 ny = fp2_neg(y);
+    const bool want = (f & 0x20) != 0;
+    out.x = x;
+    out.y = (fp2_gt(y, ny) == want) ? y : ny;
+    if (check_subgroup && !g2_in_subgroup(out.x, out.y)) return false;
+    return true;
+}
+
+// ============================================================== pairing pieces
+struct LineCoeff {
+    Fp2 c0, c1, c2;
+};
+
+// G2Prepared doubling step (Algorithm 26, eprint 2010/354; the crate's form)
+BD LineCoeff g2_doubling_step_v(G2& r) {
+    Fp2 tmp0 = fp2_sqr(r.x);
+    Fp2 tmp1 = fp2_sqr(r.y);
+    Fp2 tmp2 = fp2_sqr(tmp1);
+    Fp2 tmp3 = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr(fp2_add(tmp1, r.x)), tmp0), tmp2));
+    const Fp2 tmp4 = fp2_add(fp2_dbl(tmp0), tmp0);
+    Fp2 tmp6 = fp2_add(r.x, tmp4);
+    const Fp2 tmp5 = fp2_sqr(tmp4);
+    const Fp2 zsq = fp2_sqr(r.z);
+    r.x = fp2_sub(fp2_sub(tmp5, tmp3), tmp3);
+    r.z = fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.z, r.y)), tmp1), zsq);
+    r.y = fp2_mul(fp2_sub(tmp3, r.x), tmp4);
+    tmp2 = fp2_dbl(fp2_dbl(fp2_dbl(tmp2)));
+    r.y = fp2_sub(r.y, tmp2);
+    tmp3 = fp2_neg(fp2_dbl(fp2_mul(tmp4, zsq)));
+    tmp6 = fp2_sub(fp2_sub(fp2_sqr(tmp6), tmp0), tmp5);
+    tmp1 = fp2_dbl(fp2_dbl(tmp1));
+    tmp6 = fp2_sub(tmp6, tmp1);
+    tmp0 = fp2_dbl(fp2_mul(r.z, zsq));
+    return {tmp0, tmp3, tmp6};
+}
+
+// G2Prepared addition step (Algorithm 27)
+__device__ __noinline__ void g2_doubling_step_p(G2* r, LineCoeff* c) { *c = g2_doubling_step_v(*r); }
+BD LineCoeff g2_doubling_step(G2& r) {
+    LineCoeff c;
+    g2_doubling_step_p(&r, &c);
+    return c;
+}
+
+BD LineCoeff g2_addition_step_v(G2& r, const Fp2& qx, const Fp2& qy) {
+    const Fp2 zsq = fp2_sqr(r.z);
+    const Fp2 ysq = fp2_sqr(qy);
+    const Fp2 t0 = fp2_mul(zsq, qx);
+    const Fp2 t1 = fp2_mul(fp2_sub(fp2_sub(fp2_sqr(fp2_add(qy, r.z)), ysq), zsq), zsq);
+    const Fp2 t2 = fp2_sub(t0, r.x);
+    const Fp2 t3 = fp2_sqr(t2);
+    const Fp2 t4 = fp2_dbl(fp2_dbl(t3));
+    const Fp2 t5 = fp2_mul(t4, t2);
+    Fp2 t6 = fp2_sub(fp2_sub(t1, r.y), r.y);
+    Fp2 t9 = fp2_mul(t6, qx);
+    const Fp2 t7 = fp2_mul(t4, r.x);
+    r.x = fp2_sub(fp2_sub(fp2_sub(fp2_sqr(t6), t5), t7), t7);
+    r.z = fp2_sub(fp2_sub(fp2_sqr(fp2_add(r.z, t2)), zsq), t3);
+    Fp2 t10 = fp2_add(qy, r.z);
+    const Fp2 t8 = fp2_mul(fp2_sub(t7, r.x), t6);
+    const Fp2 tt0 = fp2_dbl(fp2_mul(r.y, t5));
+    r.y = fp2_sub(t8, tt0);
+    t10 = fp2_sub(fp2_sqr(t10), ysq);
+    const Fp2 ztsq = fp2_sqr(r.z);
+    t10 = fp2_sub(t10, ztsq);
+    t9 = fp2_sub(fp2_dbl(t9), t10);
+    t10 = fp2_dbl(r.z);
+    t6 = fp2_neg(t6);
+    const Fp2 tt1 = fp2_dbl(t6);
+    return {t10, tt1, t9};
+}
+
+__device__ __noinline__ void g2_addition_step_p(G2* r, LineCoeff* c, const Fp2* qx, const Fp2* qy) {
+    *c = g2_addition_step_v(*r, *qx, *qy);
+}
+BD LineCoeff g2_addition_step(G2& r, const Fp2& qx, const Fp2& qy) {
+    LineCoeff c;
+    g2_addition_step_p(&r, &c, &qx, &qy);
+    return c;
+}
+
+// number of line coefficients in a G2Prepared: 63 doublings after the leading
+// bit of |x|>>1 ... (bits of |x|>>1 below its top bit) + additions + final doubling
+constexpr int kMillerSteps = 68;
+
+// ell(f, coeffs, p) of the crate, in place
+BD void ell(Fp12* f, const LineCoeff& c, const Fp& px, const Fp& py) {
+    const Fp2 c1 = fp2_mul_fp(c.c1, px), c4 = fp2_mul_fp(c.c0, py);
+    fp12_mul_by_014_p(f, &c.c2, &c1, &c4);
+}
+
+// the crate's final_exponentiation, in place
+__device__ __noinline__ void final_exponentiation(Fp12* io) {
+    Fp12 r, f1, f2, y0, y1, y2, y3;
+    f1 = fp12_conj(*io);
+    fp12_inv_p(&f2, io);
+    fp12_mul_p(&r, &f1, &f2);
+    f2 = r;
+    fp12_frob_p<2>(&r, &r);
+    fp12_mul_p(&r, &r, &f2);
+    fp12_cyc_sqr_p(&y0, &r);
+    y1 = y0;
+    fp12_exp_by_x_inplace(&y1);
+    y2 = y1;
+    fp12_cyc_pow_conj(&y2, kBlsX >> 1, 62);  // conj(y1^(|x|>>1))
+    y3 = fp12_conj(r);
+    fp12_mul_p(&y1, &y1, &y3);
+    y1 = fp12_conj(y1);
+    fp12_mul_p(&y1, &y1, &y2);
+    y2 = y1;
+    fp12_exp_by_x_inplace(&y2);
+    y3 = y2;
+    fp12_exp_by_x_inplace(&y3);
+    y1 = fp12_conj(y1);
+    fp12_mul_p(&y3, &y3, &y1);
+    y1 = fp12_conj(y1);
+    fp12_frob_p<3>(&y1, &y1);
+    fp12_frob_p<2>(&y2, &y2);
+    fp12_mul_p(&y1, &y1, &y2);
+    y2 = y3;
+    fp12_exp_by_x_inplace(&y2);
+    fp12_mul_p(&y2, &y2, &y0);
+    fp12_mul_p(&y2, &y2, &r);
+    fp12_mul_p(&y1, &y1, &y2);
+    fp12_frob_p<1>(&y2, &y3);
+    fp12_mul_p(io, &y1, &y2);
+}
+
+#undef BD
+
+}  // namespace bls
+}  // namespace hbg

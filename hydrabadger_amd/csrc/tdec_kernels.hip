@@ -1,0 +1,603 @@
+// tdec_kernels.hip — gfx950 kernels for hbbft's ThresholdDecrypt path (family 3).
+//
+// Restates threshold_crypto [EXT] as hbbft's ThresholdDecrypt drives it
+// (reached from /root/reference/src/hydrabadger/
+// state.rs:486-487):
+//   tdec_ct_prepare     per ciphertext: decompress + subgroup-check U (G1) and
+//                       W (G2), H = hash_g1_g2(U, V) (SHA3 -> ChaChaRng ->
+//                       try-and-increment -> cofactor), G2Prepared lines of H, W
+//   tdec_pk_prepare     PublicKeyShare table: decompress + subgroup check
+//   tdec_verify_shares  PublicKeyShare::verify_decryption_share for every share:
+//                       e(S_i, H) * e(-PK_i, W) == 1 (one 2-pair Miller loop +
+//                       one final exponentiation per work-item)
+//   tdec_ct_verify      Ciphertext::verify: e(G1, W) * e(-U, H) == 1
+//   tdec_combine        PublicKeySet::decrypt: interpolate the first t+1 shares
+//                       at 0 (Lagrange over Fr) + xor_with_hash
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bls.h"
+#include "keccak.h"
+#include "tdec_kernels.h"
+
+namespace hbg {
+namespace bls {
+
+#define BD __device__ __forceinline__
+
+// ------------------------------------------------------------------ SHA3-256 over bytes
+BD void sha3_bytes(const uint8_t* p, uint32_t len, uint8_t out[32]) {
+    u64p a[25];
+    keccak_zero(a);
+    uint32_t pos = 0;
+    while (true) {
+        const uint32_t take = (len - pos) >= 136 ? 136 : (len - pos);
+        uint8_t blk[136];
+        for (uint32_t i = 0; i < 136; ++i) blk[i] = i < take ? p[pos + i] : 0;
+        const bool last = take < 136;
+        if (last) {
+            blk[take] ^= 0x06;
+            blk[135] ^= 0x80;
+        }
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                lo |= (uint32_t)blk[8 * i + b] << (8 * b);
+                hi |= (uint32_t)blk[8 * i + 4 + b] << (8 * b);
+            }
+            a[i].lo ^= lo;
+            a[i].hi ^= hi;
+        }
+        keccak_f(a);
+        pos += take;
+        if (last) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            out[8 * i + b] = (uint8_t)(a[i].lo >> (8 * b));
+            out[8 * i + 4 + b] = (uint8_t)(a[i].hi >> (8 * b));
+        }
+    }
+}
+
+// ------------------------------------------------------------------ ChaCha20 (rand_chacha layout)
+BD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+#define QR(a, b, c, d)            \
+    a += b;                       \
+    d = rotl32(d ^ a, 16);        \
+    c += d;                       \
+    b = rotl32(b ^ c, 12);        \
+    a += b;                       \
+    d = rotl32(d ^ a, 8);         \
+    c += d;                       \
+    b = rotl32(b ^ c, 7);
+
+BD void chacha_block(const uint32_t key[8], uint32_t counter, uint32_t out[16]) {
+    uint32_t s[16] = {0x61707865u, 0x3320646Eu, 0x79622D32u, 0x6B206574u, key[0], key[1], key[2], key[3],
+                      key[4],      key[5],      key[6],      key[7],      counter, 0u,     0u,     0u};
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = s[i];
+    for (int r = 0; r < 10; ++r) {
+        QR(w[0], w[4], w[8], w[12]);
+        QR(w[1], w[5], w[9], w[13]);
+        QR(w[2], w[6], w[10], w[14]);
+        QR(w[3], w[7], w[11], w[15]);
+        QR(w[0], w[5], w[10], w[15]);
+        QR(w[1], w[6], w[11], w[12]);
+        QR(w[2], w[7], w[8], w[13]);
+        QR(w[3], w[4], w[9], w[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[i] = w[i] + s[i];
+}
+#undef QR
+
+struct ChaChaRng {
+    uint32_t key[8];
+    uint32_t buf[16];
+    uint32_t counter, idx;
+    BD void init(const uint8_t seed[32]) {
+        for (int i = 0; i < 8; ++i)
+            key[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) | ((uint32_t)seed[4 * i + 2] << 16) |
+                     ((uint32_t)seed[4 * i + 3] << 24);
+        counter = 0;
+        idx = 16;
+    }
+    BD uint32_t next_u32() {
+        if (idx >= 16) {
+            chacha_block(key, counter, buf);
+            ++counter;
+            idx = 0;
+        }
+        return buf[idx++];
+    }
+};
+
+// ------------------------------------------------------------------ hash_g1_g2
+// ff_derive Rand for Fq: 6 x next_u64 (LE), top limb masked by 3 shave bits,
+// rejected unless < p, taken as a Montgomery representation.  Our Montgomery
+// form of that value IS the repr (same R = 2^384).
+BD Fp rand_fq(ChaChaRng& rng) {
+    while (true) {
+        Fp r;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) r[i] = rng.next_u32();
+        r[11] &= 0x1FFFFFFFu;
+        if (fp_raw_lt_p(r)) return r;
+    }
+}
+
+// [k]P for the crate's 508-bit G2 cofactor, P affine (left-to-right double-and-add)
+__device__ __constant__ static const uint32_t gG2Cofactor[16] = {
+    kG2Cofactor[0],  kG2Cofactor[1],  kG2Cofactor[2],  kG2Cofactor[3], kG2Cofactor[4],  kG2Cofactor[5],
+    kG2Cofactor[6],  kG2Cofactor[7],  kG2Cofactor[8],  kG2Cofactor[9], kG2Cofactor[10], kG2Cofactor[11],
+    kG2Cofactor[12], kG2Cofactor[13], kG2Cofactor[14], kG2Cofactor[15]};
+
+BD G2 g2_scale_by_cofactor(const Fp2& px, const Fp2& py) {
+    G2 r = {px, py, fp2_one()};
+    const int top = 506;  // bit index of the leading one of h2 (507 bits)
+    for (int i = top - 1; i >= 0; --i) {
+        r = g2_dbl(r);
+        if ((gG2Cofactor[i >> 5] >> (i & 31)) & 1u) r = g2_add_mixed(r, px, py);
+    }
+    return r;
+}
+
+// hash_g2(digest_input) given its 32-byte SHA3 digest as the ChaCha seed.
+BD G2A hash_g2_from_seed(const uint8_t seed[32]) {
+    ChaChaRng rng;
+    rng.init(seed);
+    const Fp2 b2 = {fp_const(kB2), fp_const(kB2)};
+    while (true) {
+        Fp2 x;
+        x.c0 = rand_fq(rng);
+        x.c1 = rand_fq(rng);
+        const bool greatest = (rng.next_u32() & 1u) != 0;
+        bool ok;
+        const Fp2 y = fp2_sqrt(fp2_add(fp2_mul(fp2_sqr(x), x), b2), ok);
+        if (!ok) continue;
+        const Fp2 ny = fp2_neg(y);
+        // the crate: y if (y < negy) ^ greatest else negy
+        const bool y_lt = fp2_gt(ny, y);
+        const Fp2 yy = (y_lt != greatest) ? y : ny;
+        const G2A h = g2_to_affine(g2_scale_by_cofactor(x, yy));
+        if (!h.inf) return h;
+    }
+}
+
+// ------------------------------------------------------------------ G2Prepared
+// coeff layout per point: [68][c0.c0, c0.c1, c1.c0, c1.c1, c2.c0, c2.c1][12 u32]
+BD void store_fp(uint32_t* dst, const Fp& a) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) dst[i] = a[i];
+}
+BD Fp load_fp(const uint32_t* src) {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) r[i] = src[i];
+    return r;
+}
+BD void store_line(uint32_t* dst, const LineCoeff& c) {
+    store_fp(dst + 0, c.c0.c0);
+    store_fp(dst + 12, c.c0.c1);
+    store_fp(dst + 24, c.c1.c0);
+    store_fp(dst + 36, c.c1.c1);
+    store_fp(dst + 48, c.c2.c0);
+    store_fp(dst + 60, c.c2.c1);
+}
+BD LineCoeff load_line(const uint32_t* src) {
+    LineCoeff c;
+    c.c0 = {load_fp(src + 0), load_fp(src + 12)};
+    c.c1 = {load_fp(src + 24), load_fp(src + 36)};
+    c.c2 = {load_fp(src + 48), load_fp(src + 60)};
+    return c;
+}
+
+// |x| >> 1 = 0x6900800000008000: the 62 bits below its leading one drive the loop.
+constexpr uint64_t kXHalf = kBlsX >> 1;
+
+BD void g2_prepare(const Fp2& qx, const Fp2& qy, uint32_t* out) {
+    G2 r = {qx, qy, fp2_one()};
+    int k = 0;
+    for (int i = 61; i >= 0; --i) {
+        store_line(out + 72 * k++, g2_doubling_step(r));
+        if ((kXHalf >> i) & 1ull) store_line(out + 72 * k++, g2_addition_step(r, qx, qy));
+    }
+    store_line(out + 72 * k, g2_doubling_step(r));
+}
+
+// Miller loop over two pairs with prepared lines (the crate's miller_loop);
+// a pair is skipped when its G1 or G2 point is the identity.
+__device__ __noinline__ void miller_loop2(Fp12* out, const uint32_t* c1, Fp p1x, Fp p1y, bool use1,
+                                          const uint32_t* c2, Fp p2x, Fp p2y, bool use2) {
+    Fp12 f = fp12_one();
+    int k = 0;
+    for (int i = 61; i >= 0; --i) {
+        if (use1) ell(&f, load_line(c1 + 72 * k), p1x, p1y);
+        if (use2) ell(&f, load_line(c2 + 72 * k), p2x, p2y);
+        ++k;
+        if ((kXHalf >> i) & 1ull) {
+            if (use1) ell(&f, load_line(c1 + 72 * k), p1x, p1y);
+            if (use2) ell(&f, load_line(c2 + 72 * k), p2x, p2y);
+            ++k;
+        }
+        fp12_sqr_p(&f, &f);
+    }
+    if (use1) ell(&f, load_line(c1 + 72 * k), p1x, p1y);
+    if (use2) ell(&f, load_line(c2 + 72 * k), p2x, p2y);
+    *out = fp12_conj(f);
+}
+
+// one pairing check: prod e(P_i, Q_i) == 1 over the two prepared pairs
+BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool use1, const uint32_t* c2,
+                       const Fp& p2x, const Fp& p2y, bool use2) {
+    Fp12 f;
+    miller_loop2(&f, c1, p1x, p1y, use1, c2, p2x, p2y, use2);
+    final_exponentiation(&f);
+    return fp12_is_one(f);
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ __launch_bounds__(64) void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
+                                                      const uint8_t* __restrict__ V,
+                                                      const uint64_t* __restrict__ V_off,
+                                                      const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
+                                                      int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH,
+                                                      uint32_t* __restrict__ coefW) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int32_t st = 0;
+    G1A u;
+    G2A w;
+    if (!g1_decompress(U48 + 48ull * k, u, true)) st = HBG_E_INVALID_POINT;
+    if (!g2_decompress(W96 + 96ull * k, w, true)) st = HBG_E_INVALID_POINT;
+    uint32_t* cu = ct_u + 32ull * k;
+    store_fp(cu, u.x);
+    store_fp(cu + 12, u.y);
+    cu[24] = u.inf ? 1u : 0u;
+    cu[25] = w.inf ? 1u : 0u;
+    ct_status[k] = st;
+    if (st != 0) return;
+    // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
+    const uint64_t off = V_off[k], len = V_off[k + 1] - off;
+    uint8_t m[64 + 48];
+    uint32_t mlen;
+    if (len > 64) {
+        sha3_bytes(V + off, (uint32_t)len, m);
+        mlen = 32;
+    } else {
+        for (uint32_t i = 0; i < len; ++i) m[i] = V[off + i];
+        mlen = (uint32_t)len;
+    }
+    for (int i = 0; i < 48; ++i) m[mlen + i] = U48[48ull * k + i];
+    uint8_t seed[32];
+    sha3_bytes(m, mlen + 48, seed);
+    const G2A h = hash_g2_from_seed(seed);
+    g2_prepare(h.x, h.y, coefH + (uint64_t)k * 72 * kMillerSteps);
+    if (!w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
+}
+
+__global__ __launch_bounds__(64) void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
+                                                      uint32_t* __restrict__ pk_aff, int32_t* __restrict__ pk_status) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    G1A p;
+    const bool ok = g1_decompress(pk48 + 48ull * k, p, true);
+    uint32_t* d = pk_aff + 32ull * k;
+    store_fp(d, p.x);
+    store_fp(d + 12, p.y);
+    d[24] = p.inf ? 1u : 0u;
+    pk_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
+}
+
+__global__ __launch_bounds__(64) void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ share48,
+                                                         const uint32_t* __restrict__ share_ct,
+                                                         const uint32_t* __restrict__ share_pk,
+                                                         const uint32_t* __restrict__ ct_u,
+                                                         const int32_t* __restrict__ ct_status,
+                                                         const uint32_t* __restrict__ coefH,
+                                                         const uint32_t* __restrict__ coefW,
+                                                         const uint32_t* __restrict__ pk_aff,
+                                                         const int32_t* __restrict__ pk_status,
+                                                         uint8_t* __restrict__ ok) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t ct = share_ct[k], pk = share_pk[k];
+    bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
+    G1A s;
+    if (good) good = g1_decompress(share48 + 48ull * k, s, true);
+    if (good) {
+        const uint32_t* pa = pk_aff + 32ull * pk;
+        const Fp pkx = load_fp(pa), pky = fp_neg(load_fp(pa + 12));
+        const bool pk_inf = pa[24] != 0;
+        const bool w_inf = ct_u[32ull * ct + 25] != 0;
+        good = pairing_check2(coefH + (uint64_t)ct * 72 * kMillerSteps, s.x, s.y, !s.inf,
+                              coefW + (uint64_t)ct * 72 * kMillerSteps, pkx, pky, !pk_inf && !w_inf);
+    }
+    ok[k] = good ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
+                                                     const int32_t* __restrict__ ct_status,
+                                                     const uint32_t* __restrict__ coefH,
+                                                     const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    bool good = ct_status[k] == 0;
+    if (good) {
+        const uint32_t* cu = ct_u + 32ull * k;
+        const bool u_inf = cu[24] != 0, w_inf = cu[25] != 0;
+        const Fp ux = load_fp(cu), nuy = fp_neg(load_fp(cu + 12));
+        // e(G1, W) * e(-U, H) == 1
+        good = pairing_check2(coefW + (uint64_t)k * 72 * kMillerSteps, fp_const(kG1x), fp_const(kG1y), !w_inf,
+                              coefH + (uint64_t)k * 72 * kMillerSteps, ux, nuy, !u_inf);
+    }
+    ok[k] = good ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- Fr (scalar field) for Lagrange
+// r < 2^255, 8 x u32 limbs, Montgomery with R = 2^256 (plain C: low volume).
+struct Fr {
+    uint32_t v[8];
+};
+constexpr uint32_t kR_N0 = 0xFFFFFFFFu;  // -r^-1 mod 2^32 (r = 1 mod 2^32)
+
+BD Fr fr_mul(const Fr& a, const Fr& b) {
+    uint32_t t[10] = {0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c += (uint64_t)a.v[j] * b.v[i] + t[j];
+            t[j] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[8];
+        t[8] = (uint32_t)c;
+        t[9] = (uint32_t)(c >> 32);
+        const uint32_t m = t[0] * kR_N0;
+        c = (uint64_t)m * kR[0] + t[0];
+        c >>= 32;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            c += (uint64_t)m * kR[j] + t[j];
+            t[j - 1] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[8];
+        t[7] = (uint32_t)c;
+        t[8] = t[9] + (uint32_t)(c >> 32);
+    }
+    Fr r, u;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u.v[i] = __builtin_subc(t[i], kR[i], br, &br);
+    const bool ge = t[8] || !br;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = ge ? u.v[i] : t[i];
+    return r;
+}
+
+BD Fr fr_from_u32(uint32_t x) {  // Montgomery form of a small integer: x * R mod r = mul(x, R^2)
+    Fr a = {{x, 0, 0, 0, 0, 0, 0, 0}};
+    Fr r2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r2.v[i] = kFrR2[i];
+    return fr_mul(a, r2);
+}
+
+BD Fr fr_sub(const Fr& a, const Fr& b) {
+    Fr r, u;
+    uint32_t br = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u.v[i] = __builtin_addc(r.v[i], kR[i], c, &c);
+    return br ? u : r;
+}
+
+BD Fr fr_inv(const Fr& a) {  // a^(r-2)
+    Fr r = a;
+    for (int i = 253; i >= 0; --i) {
+        r = fr_mul(r, r);
+        if ((kRm2[i >> 5] >> (i & 31)) & 1u) r = fr_mul(r, a);
+    }
+    return r;
+}
+
+BD bool fr_is_zero(const Fr& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.v[i];
+    return o == 0;
+}
+
+BD Fr fr_canonical(const Fr& a) {
+    Fr one = {{1, 0, 0, 0, 0, 0, 0, 0}};
+    return fr_mul(a, one);
+}
+
+// PublicKeySet::decrypt for one ciphertext per work-item.
+// shares: [n][t+1][48] compressed (already verified: no subgroup re-check, as
+// in the crate where decrypt consumes parsed shares); idx: [n][t+1] node indices.
+__global__ __launch_bounds__(64) void tdec_combine(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
+                                                   const uint32_t* __restrict__ idx, const uint8_t* __restrict__ V,
+                                                   const uint64_t* __restrict__ V_off, uint8_t* __restrict__ out,
+                                                   int32_t* __restrict__ status, uint32_t* __restrict__ scratch) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t m = t + 1;
+    const uint32_t* ix = idx + (uint64_t)k * m;
+    // per-lane scratch: lambda[m][8] then points[m][24]
+    uint32_t* lam = scratch + (uint64_t)k * m * 32;
+    uint32_t* pts = lam + m * 8;
+    int32_t st = 0;
+    // duplicate indices -> DuplicateEntry (non-invertible denominator)
+    for (uint32_t i = 0; i < m && st == 0; ++i)
+        for (uint32_t j = i + 1; j < m; ++j)
+            if (ix[i] == ix[j]) st = HBG_E_DUPLICATE_ENTRY;
+    // decompress
+    for (uint32_t i = 0; i < m && st == 0; ++i) {
+        G1A p;
+        if (!g1_decompress(share48 + ((uint64_t)k * m + i) * 48, p, false)) {
+            st = HBG_E_INVALID_POINT;
+            break;
+        }
+        store_fp(pts + 24 * i, p.x);
+        store_fp(pts + 24 * i + 12, p.y);
+        // an identity share contributes nothing; mark it with a top y limb no
+        // field element can have (p's top limb is 0x1a0111ea)
+        if (p.inf) pts[24 * i + 23] = 0xFFFFFFFFu;
+    }
+    status[k] = st;
+    if (st != 0) return;
+    // lambda_i = prod_{j != i} x_j / prod_{j != i} (x_j - x_i),  x = index + 1  (mod r)
+    for (uint32_t i = 0; i < m; ++i) {
+        Fr num = fr_from_u32(1), den = fr_from_u32(1);
+        const Fr xi = fr_from_u32(ix[i] + 1);
+        for (uint32_t j = 0; j < m; ++j) {
+            if (j == i) continue;
+            const Fr xj = fr_from_u32(ix[j] + 1);
+            num = fr_mul(num, xj);
+            den = fr_mul(den, fr_sub(xj, xi));
+        }
+        const Fr l = fr_canonical(fr_mul(num, fr_inv(den)));
+#pragma unroll
+        for (int w = 0; w < 8; ++w) lam[8 * i + w] = l.v[w];
+    }
+    // sum lambda_i * S_i  (Straus, 1-bit window, shared doublings)
+    G1 acc = {fp_one(), fp_one(), fp_zero()};
+    for (int bit = 254; bit >= 0; --bit) {
+        acc = g1_dbl(acc);
+        for (uint32_t i = 0; i < m; ++i) {
+            if (pts[24 * i + 23] == 0xFFFFFFFFu) continue;
+            if ((lam[8 * i + (bit >> 5)] >> (bit & 31)) & 1u)
+                acc = g1_add_mixed(acc, load_fp(pts + 24 * i), load_fp(pts + 24 * i + 12));
+        }
+    }
+    const G1A g = g1_to_affine(acc);
+    uint8_t cg[48];
+    g1_compress(cg, g);
+    uint8_t seed[32];
+    sha3_bytes(cg, 48, seed);
+    ChaChaRng rng;
+    rng.init(seed);
+    const uint64_t off = V_off[k], len = V_off[k + 1] - off;
+    for (uint64_t i = 0; i < len; ++i) out[off + i] = V[off + i] ^ (uint8_t)(rng.next_u32() & 0xFFu);
+}
+
+// ------------------------------------------------------------------ unit-test hook
+// op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
+//     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
+// Field values cross the boundary as canonical raw limbs (12 u32 LE).
+__global__ __launch_bounds__(64) void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
+                                                uint32_t* __restrict__ out, uint32_t in_words,
+                                                uint32_t out_words, uint32_t* __restrict__ lines) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t* a = in + (uint64_t)k * in_words;
+    uint32_t* o = out + (uint64_t)k * out_words;
+    auto ld = [&](int w) { return fp_to_mont(load_fp(a + w)); };
+    auto st = [&](int w, const Fp& x) { store_fp(o + w, fp_from_mont(x)); };
+    auto st12 = [&](const Fp12& f) {
+        const Fp* c[12] = {&f.c0.c0.c0, &f.c0.c0.c1, &f.c0.c1.c0, &f.c0.c1.c1, &f.c0.c2.c0, &f.c0.c2.c1,
+                           &f.c1.c0.c0, &f.c1.c0.c1, &f.c1.c1.c0, &f.c1.c1.c1, &f.c1.c2.c0, &f.c1.c2.c1};
+        for (int i = 0; i < 12; ++i) st(12 * i, *c[i]);
+    };
+    if (op == 0) {
+        st(0, fp_mul(ld(0), ld(12)));
+    } else if (op == 1) {
+        st(0, fp_inv(ld(0)));
+    } else if (op == 2) {
+        bool ok;
+        const Fp2 r = fp2_sqrt({ld(0), ld(12)}, ok);
+        st(0, r.c0);
+        st(12, r.c1);
+        o[24] = ok;
+    } else if (op == 3) {
+        G1A p;
+        const bool ok = g1_decompress(reinterpret_cast<const uint8_t*>(a), p, true);
+        st(0, p.x);
+        st(12, p.y);
+        o[24] = ok;
+        o[25] = p.inf;
+    } else if (op == 4) {
+        G2A p;
+        const bool ok = g2_decompress(reinterpret_cast<const uint8_t*>(a), p, true);
+        st(0, p.x.c0);
+        st(12, p.x.c1);
+        st(24, p.y.c0);
+        st(36, p.y.c1);
+        o[48] = ok;
+        o[49] = p.inf;
+    } else if (op == 5 || op == 7) {
+        // in: P.x P.y Q.x0 Q.x1 Q.y0 Q.y1 (canonical affine)
+        uint32_t* ln = lines + (uint64_t)k * 72 * kMillerSteps;
+        g2_prepare({ld(24), ld(36)}, {ld(48), ld(60)}, ln);
+        Fp12 f;
+        miller_loop2(&f, ln, ld(0), ld(12), true, ln, ld(0), ld(12), false);
+        if (op == 5) final_exponentiation(&f);
+        st12(f);
+    } else if (op == 6) {
+        const G2A h = hash_g2_from_seed(reinterpret_cast<const uint8_t*>(a));
+        st(0, h.x.c0);
+        st(12, h.x.c1);
+        st(24, h.y.c0);
+        st(36, h.y.c1);
+    } else if (op == 8) {
+        Fp12 f;
+        Fp* c[12] = {&f.c0.c0.c0, &f.c0.c0.c1, &f.c0.c1.c0, &f.c0.c1.c1, &f.c0.c2.c0, &f.c0.c2.c1,
+                     &f.c1.c0.c0, &f.c1.c0.c1, &f.c1.c1.c0, &f.c1.c1.c1, &f.c1.c2.c0, &f.c1.c2.c1};
+        for (int i = 0; i < 12; ++i) *c[i] = ld(12 * i);
+        final_exponentiation(&f);
+        st12(f);
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                                  const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
+                                  uint32_t* coefW, hipStream_t st) {
+    tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, W96, ct_u, ct_status, coefH, coefW);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
+                                  hipStream_t st) {
+    tdec_pk_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, pk48, pk_aff, pk_status);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_verify_shares(uint64_t n, const uint8_t* share48, const uint32_t* share_ct,
+                                     const uint32_t* share_pk, const uint32_t* ct_u, const int32_t* ct_status,
+                                     const uint32_t* coefH, const uint32_t* coefW, const uint32_t* pk_aff,
+                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st) {
+    tdec_verify_shares<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(
+        n, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
+                                 const uint32_t* coefW, uint8_t* ok, hipStream_t st) {
+    tdec_ct_verify<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, ct_u, ct_status, coefH, coefW, ok);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
+                               const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
+                               uint32_t* scratch, hipStream_t st) {
+    tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status, scratch);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,
+                            uint32_t out_words, uint32_t* lines, hipStream_t st) {
+    tdec_test<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(op, n, in, out, in_words, out_words, lines);
+    return hipGetLastError();
+}
+
+#undef BD
+}  // namespace bls
+}  // namespace hbg

@@ -1,0 +1,134 @@
+"""Drop-in mirror of threshold_crypto's ThresholdDecrypt surfaces over the gfx950 engine.
+
+Same names, argument meaning and error behaviour as threshold_crypto [EXT]
+as hbbft's ``ThresholdDecrypt`` uses it, reached from
+``/root/reference/src/hydrabadger/state.rs:486-487``:
+
+  Ciphertext(U, V, W).verify()                         -> hbg_ct_verify          (a12)
+  PublicKeyShare.verify_decryption_share(share, ct)    -> hbg_tdec_verify_shares (a14)
+  PublicKeySet.decrypt(shares, ct)                     -> hbg_tdec_combine       (a15, a16)
+
+Points are the crate's zcash-compressed bytes (G1 48 B, G2 96 B).  Every
+computation runs in libhbgpu.so on the GPU; there is no CPU fallback.  The
+``*_batch`` forms take whole epochs at once.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import HbgError, check, default_context, lib, ptr
+
+
+class NotEnoughShares(HbgError):
+    def __init__(self):
+        RuntimeError.__init__(self, "NotEnoughShares")
+        self.code = _lib.HBG_E_NOT_ENOUGH_SHARES
+
+
+class DuplicateEntry(HbgError):
+    pass
+
+
+@dataclass
+class Ciphertext:
+    U: bytes  # G1, 48 B compressed
+    V: bytes
+    W: bytes  # G2, 96 B compressed
+
+    def verify(self, ctx=None) -> bool:
+        return bool(ct_verify_batch([self], ctx)[0])
+
+
+def _ct_table(cts):
+    n = len(cts)
+    U = np.frombuffer(b"".join(bytes(c.U) for c in cts), np.uint8).copy().reshape(n, 48)
+    W = np.frombuffer(b"".join(bytes(c.W) for c in cts), np.uint8).copy().reshape(n, 96)
+    lens = [len(c.V) for c in cts]
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    V = np.frombuffer(b"".join(bytes(c.V) for c in cts) or b"\0", np.uint8).copy()
+    return U, V, off, W
+
+
+def ct_verify_batch(cts: list, ctx=None) -> np.ndarray:
+    n = len(cts)
+    if n == 0:
+        return np.zeros(0, np.uint8)
+    U, V, off, W = _ct_table(cts)
+    ok = np.zeros(n, np.uint8)
+    check(lib().hbg_ct_verify((ctx or default_context()).h, n, ptr(U), ptr(V), ptr(off), ptr(W), ptr(ok), 0),
+          "Ciphertext::verify")
+    return ok
+
+
+def verify_shares_batch(cts: list, pk_shares: list, shares: list, ctx=None) -> np.ndarray:
+    """shares: [(share48, ct_index, pk_index)] -> ok bits (one per share)."""
+    n = len(shares)
+    if n == 0:
+        return np.zeros(0, np.uint8)
+    U, V, off, W = _ct_table(cts)
+    pk = np.frombuffer(b"".join(bytes(p) for p in pk_shares), np.uint8).copy().reshape(len(pk_shares), 48)
+    sh = np.frombuffer(b"".join(bytes(s) for s, _, _ in shares), np.uint8).copy().reshape(n, 48)
+    sct = np.array([c for _, c, _ in shares], np.uint32)
+    spk = np.array([p for _, _, p in shares], np.uint32)
+    ok = np.zeros(n, np.uint8)
+    check(lib().hbg_tdec_verify_shares((ctx or default_context()).h, len(cts), ptr(U), ptr(V), ptr(off), ptr(W),
+                                       len(pk_shares), ptr(pk), n, ptr(sh), ptr(sct), ptr(spk), ptr(ok), 0),
+          "verify_decryption_share")
+    return ok
+
+
+@dataclass
+class PublicKeyShare:
+    pk: bytes  # 48 B compressed G1
+
+    def verify_decryption_share(self, share: bytes, ct: Ciphertext, ctx=None) -> bool:
+        return bool(verify_shares_batch([ct], [self.pk], [(share, 0, 0)], ctx)[0])
+
+
+def combine_batch(t: int, cts: list, shares: list, ctx=None):
+    """shares[k] = the first t+1 (index, share48) items for ciphertext k.
+    Returns (plaintexts, status array)."""
+    n = len(cts)
+    m = t + 1
+    for s in shares:
+        if len(s) < m:
+            raise NotEnoughShares()
+    _, V, off, _ = _ct_table(cts)
+    sh = np.frombuffer(b"".join(bytes(x) for s in shares for _, x in s[:m]), np.uint8).copy().reshape(n, m, 48)
+    ix = np.array([[i for i, _ in s[:m]] for s in shares], np.uint32).reshape(n, m)
+    out = np.zeros(max(int(off[-1]), 1), np.uint8)
+    st = np.zeros(n, np.int32)
+    check(lib().hbg_tdec_combine((ctx or default_context()).h, t, n, ptr(sh), ptr(ix), ptr(V), ptr(off), ptr(out),
+                                 ptr(st), 0), "PublicKeySet::decrypt")
+    return [out[int(off[k]):int(off[k + 1])].tobytes() for k in range(n)], st
+
+
+@dataclass
+class PublicKeySet:
+    threshold: int
+
+    def decrypt(self, shares, ct: Ciphertext, ctx=None) -> bytes:
+        """shares: iterable of (node index, share48) in iterator order."""
+        items = list(shares)
+        if len(items) <= self.threshold:
+            raise NotEnoughShares()
+        pts, st = combine_batch(self.threshold, [ct], [items[: self.threshold + 1]], ctx)
+        if st[0] == _lib.HBG_E_DUPLICATE_ENTRY:
+            raise DuplicateEntry(int(st[0]), "PublicKeySet::decrypt")
+        if st[0] != 0:
+            raise HbgError(int(st[0]), "PublicKeySet::decrypt")
+        return pts[0]
+
+
+def test_bls(op: int, inputs: np.ndarray, out_words: int, ctx=None) -> np.ndarray:
+    """Unit-test hook (include/hbgpu_testing.h): inputs [n][in_words] u32."""
+    inputs = np.ascontiguousarray(inputs, dtype=np.uint32)
+    n, iw = inputs.shape
+    out = np.zeros((n, out_words), np.uint32)
+    check(lib().hbg_test_bls((ctx or default_context()).h, op, n, ptr(inputs), iw, ptr(out), out_words),
+          "hbg_test_bls")
+    return out

@@ -136,6 +136,40 @@ int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards
                    uint8_t *payload_out, uint64_t payload_stride, uint64_t *payload_len,
                    uint8_t *status, uint64_t n, uint32_t flags);
 
+/* ---- ThresholdDecrypt (family 3): threshold_crypto surfaces ----------------
+ * Points cross the boundary in the zcash compressed encoding the crate
+ * serialises (G1 48 B, G2 96 B).  A ciphertext table of n_ct entries is
+ * U48 [n_ct][48], W96 [n_ct][96] and the V byte strings concatenated in V with
+ * V_off[n_ct + 1] offsets (entry k = V[V_off[k] .. V_off[k+1])).
+ */
+
+/* PublicKeyShare::verify_decryption_share for n_shares shares:
+ * share k (share48[k]) claims to decrypt ciphertext share_ct[k] under public
+ * key share pk48[share_pk[k]] (PublicKeySet::public_key_share(i) values).
+ * ok[k] = 1 iff every point decodes (in its subgroup), the ciphertext decodes,
+ * and e(share, hash_g1_g2(U, V)) == e(pk, W).  Bit-identical to the crate's
+ * bool for points the crate would deserialise. */
+int hbg_tdec_verify_shares(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, const uint8_t *V,
+                           const uint64_t *V_off, const uint8_t *W96, uint32_t n_pk,
+                           const uint8_t *pk48, uint64_t n_shares, const uint8_t *share48,
+                           const uint32_t *share_ct, const uint32_t *share_pk, uint8_t *ok,
+                           uint32_t flags);
+
+/* Ciphertext::verify for n_ct ciphertexts: ok[k] = e(G1, W) == e(U, hash_g1_g2(U, V)). */
+int hbg_ct_verify(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, const uint8_t *V,
+                  const uint64_t *V_off, const uint8_t *W96, uint8_t *ok, uint32_t flags);
+
+/* PublicKeySet::decrypt for n_ct ciphertexts with threshold t: shares48
+ * [n_ct][t+1][48] and share_index [n_ct][t+1] are the FIRST t+1 (node index,
+ * share) items in the caller's iterator order (hbbft: BTreeMap by node id);
+ * x = index + 1.  plaintext gets xor_with_hash(interpolate(...), V) at the V
+ * layout (same V_off).  status[k] = 0, HBG_E_DUPLICATE_ENTRY or
+ * HBG_E_INVALID_POINT.  Fewer than t+1 shares is the caller's
+ * NotEnoughShares (not representable in this layout). */
+int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *share48,
+                     const uint32_t *share_index, const uint8_t *V, const uint64_t *V_off,
+                     uint8_t *plaintext, int32_t *status, uint32_t flags);
+
 /* Device-side seeded generator: row k of out gets nbytes of
  * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */
 int hbg_synth_bytes(hbg_ctx *ctx, uint32_t tag, uint64_t first_instance, uint64_t nbytes,

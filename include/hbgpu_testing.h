@@ -1,0 +1,19 @@
+/* hbgpu_testing.h — unit-test hook of libhbgpu.so (not part of the drop-in
+ * surface): runs one BLS12-381 building block per item on the device so the
+ * parity tests can pin each layer against the oracle.
+ * op: 0 fp_mul  1 fp_inv  2 fp2_sqrt  3 g1_decompress  4 g2_decompress
+ *     5 pairing  6 hash_g2(seed)  7 miller_loop  8 final_exponentiation
+ * in/out: [n][in_words] / [n][out_words] u32, field values canonical LE limbs. */
+#ifndef HBGPU_TESTING_H
+#define HBGPU_TESTING_H
+#include <stdint.h>
+#include "hbgpu.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+int hbg_test_bls(hbg_ctx *ctx, int op, uint32_t n, const uint32_t *in, uint32_t in_words, uint32_t *out,
+                 uint32_t out_words);
+#ifdef __cplusplus
+}
+#endif
+#endif

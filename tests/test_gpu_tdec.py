@@ -1,0 +1,240 @@
+"""GPU parity tests for the ThresholdDecrypt path (family 3), through the C ABI.
+
+Layer by layer against the oracle (oracle/bls12_381.py, oracle/tcrypto.py):
+field mul / inverse / Fq2 sqrt, G1 / G2 decompression with subgroup checks,
+the crate's Miller loop, final exponentiation and pairing (exact Fq12 values),
+hash_g2, then the drop-in surfaces: verify_decryption_share bits (valid,
+corrupted, wrong-key, invalid encodings), Ciphertext::verify, and
+PublicKeySet::decrypt plaintexts incl. DuplicateEntry.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as B
+from oracle import tcrypto as T
+from oracle.chacha import ChaChaRng
+from tests.tdec_fixtures import from_limbs, limbs, scenario
+
+pytestmark = pytest.mark.gpu
+
+
+def _th():
+    from hydrabadger_amd import threshold as th
+    return th
+
+
+def _rnd(seed):
+    r = random.Random(seed)
+    return lambda: r.randrange(B.P)
+
+
+def test_fp_mul_inv():
+    th = _th()
+    rnd = _rnd(1)
+    vals = [(rnd(), rnd()) for _ in range(200)] + [(0, 5), (B.P - 1, B.P - 1), (1, 1)]
+    inp = np.array([limbs(a) + limbs(b) for a, b in vals], np.uint32)
+    out = th.test_bls(0, inp, 12)
+    for (a, b), o in zip(vals, out):
+        assert from_limbs(o) == a * b % B.P
+    inv_in = np.array([limbs(a) + [0] * 12 for a, _ in vals if a], np.uint32)
+    out = th.test_bls(1, inv_in, 12)
+    for row, o in zip(inv_in, out):
+        a = from_limbs(row[:12])
+        assert from_limbs(o) == pow(a, B.P - 2, B.P)
+
+
+def test_fp2_sqrt():
+    th = _th()
+    rnd = _rnd(2)
+    xs = [(rnd(), rnd()) for _ in range(40)]
+    sq = [B.f2_sqr(x) for x in xs]
+    nonsq = []
+    while len(nonsq) < 10:
+        c = (rnd(), rnd())
+        if B.f2_sqrt(c) is None:
+            nonsq.append(c)
+    vals = sq + nonsq
+    out = th.test_bls(2, np.array([limbs(a) + limbs(b) for a, b in vals], np.uint32), 25)
+    for i, (v, o) in enumerate(zip(vals, out)):
+        if i < len(sq):
+            assert o[24] == 1
+            r = (from_limbs(o[:12]), from_limbs(o[12:24]))
+            assert B.f2_sqr(r) == v
+        else:
+            assert o[24] == 0
+
+
+def _g1_words(b: bytes):
+    return list(np.frombuffer(b.ljust(48, b"\0"), np.uint32))
+
+
+def test_g1_decompress_and_subgroup():
+    th = _th()
+    pts = [B.g1_mul(B.G1, k) for k in (1, 2, 3, 77, 2 ** 200 + 5)]
+    encs = [B.g1_compress(p) for p in pts] + [B.g1_compress(None)]
+    # on the curve but outside G1
+    x = 5
+    while B.fq_sqrt((x ** 3 + 4) % B.P) is None:
+        x += 1
+    y = B.fq_sqrt((x ** 3 + 4) % B.P)
+    bad_sub = bytearray(x.to_bytes(48, "big"))
+    bad_sub[0] |= 0x80
+    not_curve = bytearray((3).to_bytes(48, "big"))
+    not_curve[0] |= 0x80
+    if B.fq_sqrt((27 + 4) % B.P) is not None:
+        not_curve = bytearray((4).to_bytes(48, "big")); not_curve[0] |= 0x80
+    no_flag = bytearray(B.g1_compress(pts[0]))
+    no_flag[0] &= 0x7F
+    encs += [bytes(bad_sub), bytes(not_curve), bytes(no_flag)]
+    out = th.test_bls(3, np.array([_g1_words(e) for e in encs], np.uint32), 26)
+    for i, p in enumerate(pts):
+        assert out[i][24] == 1 and (from_limbs(out[i][:12]), from_limbs(out[i][12:24])) == p
+    assert out[len(pts)][24] == 1 and out[len(pts)][25] == 1
+    assert [int(o[24]) for o in out[len(pts) + 1:]] == [0, 0, 0]
+    assert y is not None
+
+
+def test_g2_decompress_and_subgroup():
+    th = _th()
+    pts = [B.g2_mul(B.G2, k) for k in (1, 5, 1234567)]
+    encs = [B.g2_compress(p) for p in pts]
+    tampered = bytearray(encs[0])
+    tampered[50] ^= 1  # different x: almost surely off-curve or outside G2
+    encs.append(bytes(tampered))
+    out = th.test_bls(4, np.array([list(np.frombuffer(e, np.uint32)) for e in encs], np.uint32), 50)
+    for i, p in enumerate(pts):
+        assert out[i][48] == 1
+        got = ((from_limbs(out[i][0:12]), from_limbs(out[i][12:24])), (from_limbs(out[i][24:36]),
+                                                                       from_limbs(out[i][36:48])))
+        assert got == p
+    try:
+        B.g2_decompress(bytes(tampered))
+        ref_ok = 1
+    except ValueError:
+        ref_ok = 0
+    assert out[3][48] == ref_ok
+
+
+def _f12_from_words(o):
+    c = [from_limbs(o[12 * i:12 * i + 12]) for i in range(12)]
+    return (((c[0], c[1]), (c[2], c[3]), (c[4], c[5])), ((c[6], c[7]), (c[8], c[9]), (c[10], c[11])))
+
+
+def _pq_words(p, q):
+    return limbs(p[0]) + limbs(p[1]) + limbs(q[0][0]) + limbs(q[0][1]) + limbs(q[1][0]) + limbs(q[1][1])
+
+
+def test_miller_loop_final_exp_pairing_exact():
+    th = _th()
+    pairs = [(B.G1, B.G2), (B.g1_mul(B.G1, 9), B.g2_mul(B.G2, 11)), (B.g1_mul(B.G1, 2 ** 100 + 3), B.G2)]
+    inp = np.array([_pq_words(p, q) for p, q in pairs], np.uint32)
+    ml = th.test_bls(7, inp, 144)
+    for (p, q), o in zip(pairs, ml):
+        assert _f12_from_words(o) == B.miller_loop([(p, B.g2_prepare(q))])
+    pe = th.test_bls(5, inp, 144)
+    for (p, q), o in zip(pairs, pe):
+        assert _f12_from_words(o) == B.pairing(p, q)
+    fe = th.test_bls(8, ml, 144)
+    for o, m in zip(fe, ml):
+        assert _f12_from_words(o) == B.final_exponentiation(_f12_from_words(m))
+
+
+def test_hash_g2_from_seed():
+    th = _th()
+    from oracle.merkle import sha3
+    seeds = [sha3(bytes([i]) * i) for i in range(6)]
+    out = th.test_bls(6, np.array([list(np.frombuffer(s, np.uint32)) for s in seeds], np.uint32), 48)
+    for s, o in zip(seeds, out):
+        ref = T._rand_g2(ChaChaRng(s))
+        got = ((from_limbs(o[0:12]), from_limbs(o[12:24])), (from_limbs(o[24:36]), from_limbs(o[36:48])))
+        assert got == ref
+
+
+def _gpu_cts(th, cts):
+    return [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in cts]
+
+
+def test_verify_shares_matches_oracle():
+    th = _th()
+    s = scenario()
+    n = len(s["pk_shares"])
+    cts = _gpu_cts(th, s["cts"])
+    pk = [B.g1_compress(p) for p in s["pk_shares"]]
+    items, ref = [], []
+    for c, ct in enumerate(s["cts"]):
+        h = T.hash_g1_g2(ct.U, ct.V)
+        for i in range(n):
+            items.append((B.g1_compress(s["shares"][c][i]), c, i))
+            ref.append(True)
+        # corrupted share, wrong key index, identity share, share of another ct
+        bad = B.g1_add(s["shares"][c][0], B.G1)
+        items.append((B.g1_compress(bad), c, 0))
+        ref.append(T.verify_decryption_share(s["pk_shares"][0], bad, ct, h))
+        items.append((B.g1_compress(s["shares"][c][1]), c, 2))
+        ref.append(False)
+        items.append((B.g1_compress(None), c, 3))
+        ref.append(T.verify_decryption_share(s["pk_shares"][3], None, ct, h))
+        other = (c + 1) % len(s["cts"])
+        items.append((B.g1_compress(s["shares"][other][4]), c, 4))
+        ref.append(False)
+    # invalid encoding
+    junk = bytearray(B.g1_compress(s["shares"][0][5]))
+    junk[0] &= 0x7F
+    items.append((bytes(junk), 0, 5))
+    ref.append(False)
+    ok = th.verify_shares_batch(cts, pk, items)
+    assert ok.tolist() == [int(r) for r in ref]
+
+
+def test_ct_verify_matches_oracle():
+    th = _th()
+    s = scenario()
+    cts = list(s["cts"])
+    tampered = T.Ciphertext(cts[0].U, cts[0].V, B.g2_mul(cts[0].W, 3))
+    vt = T.Ciphertext(cts[1].U, bytes([cts[1].V[0] ^ 1]) + cts[1].V[1:], cts[1].W)
+    allc = cts + [tampered, vt]
+    ok = th.ct_verify_batch(_gpu_cts(th, allc))
+    assert ok.tolist() == [int(c.verify()) for c in allc]
+
+
+def test_combine_matches_oracle():
+    th = _th()
+    s = scenario()
+    t = s["t"]
+    cts = _gpu_cts(th, s["cts"])
+    pks = th.PublicKeySet(t)
+    for c, ct in enumerate(s["cts"]):
+        for start in (0, 2, len(s["pk_shares"]) - t - 1):
+            items = [(i, B.g1_compress(s["shares"][c][i])) for i in range(start, start + t + 1)]
+            got = pks.decrypt(items, cts[c])
+            ref = T.decrypt(t, [(i, s["shares"][c][i]) for i in range(start, start + t + 1)], ct)
+            assert got == ref == s["msgs"][c]
+    with pytest.raises(th.NotEnoughShares):
+        pks.decrypt([(0, B.g1_compress(s["shares"][0][0]))], cts[0])
+    dup = [(1, B.g1_compress(s["shares"][0][1]))] * (t + 1)
+    with pytest.raises(th.DuplicateEntry):
+        pks.decrypt(dup, cts[0])
+
+
+def test_golden_tdec_on_gpu():
+    """The committed fixture (tests/golden/tdec_golden.json) verifies and
+    decrypts on the device without recomputing anything in Python."""
+    import json
+    import os
+    th = _th()
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tdec_golden.json")))
+    sc = g["scenario"]
+    cts = [th.Ciphertext(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in sc["cts"]]
+    pk = [bytes.fromhex(p) for p in sc["pk_shares"]]
+    items = [(bytes.fromhex(sh), k, i) for k, c in enumerate(sc["cts"]) for i, sh in enumerate(c["shares"])]
+    assert th.verify_shares_batch(cts, pk, items).all()
+    assert th.ct_verify_batch(cts).all()
+    t = sc["t"]
+    pts, st = th.combine_batch(t, cts, [[(i, bytes.fromhex(x)) for i, x in enumerate(c["shares"])][:t + 1]
+                                        for c in sc["cts"]])
+    assert st.tolist() == [0] * len(cts)
+    assert [p.hex() for p in pts] == [c["plaintext"] for c in sc["cts"]]

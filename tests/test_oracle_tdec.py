@@ -1,0 +1,91 @@
+"""Pins the BLS12-381 / threshold_crypto oracle (CPU) against known answers
+(SURVEY.md §8(c)): curve constants and generators, RFC 8439 ChaCha20, the
+crate's final-exponentiation chain (= plain exponentiation cubed), pairing
+bilinearity / non-degeneracy, and encrypt -> share -> verify -> combine round
+trips.  hash_g2 itself is "parity unpinned" (version-dependent)."""
+from __future__ import annotations
+
+import json
+import os
+
+import pytest
+
+from oracle import bls12_381 as B
+from oracle import chacha
+from oracle import tcrypto as T
+from tests.tdec_fixtures import scenario
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "tdec_golden.json")
+
+
+def test_constants():
+    x = -B.BLS_X
+    assert x ** 4 - x ** 2 + 1 == B.R
+    assert (x - 1) ** 2 * B.R % 3 == 0 and (x - 1) ** 2 * B.R // 3 + x == B.P
+    assert B.g1_on_curve(B.G1) and B.g2_on_curve(B.G2)
+    assert B.g1_mul(B.G1, B.R) is None and B.g2_mul(B.G2, B.R) is None
+    assert B.g1_compress(B.G1).hex().startswith("97f1d3a73197d794")
+    h2 = (x ** 8 - 4 * x ** 7 + 5 * x ** 6 - 4 * x ** 4 + 6 * x ** 3 - 4 * x ** 2 - 4 * x + 13) // 9
+    assert h2 == B.G2_COFACTOR
+
+
+def test_chacha_rfc8439_block():
+    w = chacha.block(bytes(range(32)), 1, bytes.fromhex("000000090000004a00000000"))
+    assert w[0] == 0xE4E7F110 and w[1] == 0x15593BD1 and w[15] == 0x4E3C50A2
+
+
+def test_compression_roundtrip():
+    for k in (1, 2, 12345):
+        p = B.g1_mul(B.G1, k)
+        assert B.g1_decompress(B.g1_compress(p)) == p
+        q = B.g2_mul(B.G2, k)
+        assert B.g2_decompress(B.g2_compress(q)) == q
+
+
+def test_pairing_bilinear_and_chain():
+    e = B.pairing(B.G1, B.G2)
+    assert e != B.F12_ONE
+    assert B.pairing(B.g1_mul(B.G1, 6), B.g2_mul(B.G2, 7)) == B.f12_pow(e, 42)
+    f = B.miller_loop([(B.G1, B.g2_prepare(B.G2))])
+    assert B.final_exponentiation(f) == B.f12_pow(B.final_exponentiation_plain(f), 3)
+    assert B.f12_pow(e, B.R) == B.F12_ONE
+
+
+def test_threshold_roundtrip_and_negatives():
+    s = scenario()
+    t, ct = s["t"], s["cts"][0]
+    assert ct.verify()
+    h = T.hash_g1_g2(ct.U, ct.V)
+    for i, sh in enumerate(s["shares"][0]):
+        assert T.verify_decryption_share(s["pk_shares"][i], sh, ct, h)
+    bad = B.g1_add(s["shares"][0][1], B.G1)
+    assert not T.verify_decryption_share(s["pk_shares"][1], bad, ct, h)
+    assert not T.verify_decryption_share(s["pk_shares"][2], s["shares"][0][1], ct, h)  # wrong key
+    items = list(enumerate(s["shares"][0]))
+    assert T.decrypt(t, items[3:], ct) == s["msgs"][0]
+    assert T.decrypt(t, items[:t + 1], ct) == s["msgs"][0]
+    with pytest.raises(T.NotEnoughShares):
+        T.decrypt(t, items[:t], ct)
+    tampered = T.Ciphertext(ct.U, ct.V, B.g2_mul(ct.W, 2))
+    assert not tampered.verify()
+
+
+def test_hash_g2_is_in_g2():
+    for m in (b"", b"abc", bytes(100)):
+        h = T.hash_g2(m)
+        assert B.g2_on_curve(h) and B.g2_mul(h, B.R) is None
+
+
+def test_golden_tdec_reproduces():
+    with open(GOLDEN) as f:
+        g = json.load(f)
+    for case in g["hash_g2"]:
+        assert B.g2_compress(T.hash_g2(bytes.fromhex(case["msg"]))).hex() == case["point"]
+    s = scenario(**g["scenario"]["params"])
+    sc = g["scenario"]
+    assert [B.g1_compress(p).hex() for p in s["pk_shares"]] == sc["pk_shares"]
+    for k, ct in enumerate(s["cts"]):
+        c = sc["cts"][k]
+        assert (B.g1_compress(ct.U).hex(), ct.V.hex(), B.g2_compress(ct.W).hex()) == (c["U"], c["V"], c["W"])
+        assert [B.g1_compress(x).hex() for x in s["shares"][k]] == c["shares"]
+        assert s["msgs"][k].hex() == c["plaintext"]
