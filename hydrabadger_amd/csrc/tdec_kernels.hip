@@ -123,14 +123,18 @@ struct ChaChaRng {
 // ff_derive Rand for Fq: 6 x next_u64 (LE), top limb masked by 3 shave bits,
 // rejected unless < p, taken as a Montgomery representation.  Our Montgomery
 // form of that value IS the repr (same R = 2^384).
+// Bounded: each try succeeds with probability p / 2^381 > 0.8, so 64 failed
+// tries (probability < 2^-148) never happen; the bound only guarantees that
+// every wave terminates.
 BD Fp rand_fq(ChaChaRng& rng) {
-    while (true) {
-        Fp r;
+    Fp r;
+    for (int tries = 0; tries < 64; ++tries) {
 #pragma unroll
         for (int i = 0; i < 12; ++i) r[i] = rng.next_u32();
         r[11] &= 0x1FFFFFFFu;
         if (fp_raw_lt_p(r)) return r;
     }
+    return fp_zero();
 }
 
 // [k]P for the crate's 508-bit G2 cofactor, P affine (left-to-right double-and-add)
@@ -154,7 +158,9 @@ BD G2A hash_g2_from_seed(const uint8_t seed[32]) {
     ChaChaRng rng;
     rng.init(seed);
     const Fp2 b2 = {fp_const(kB2), fp_const(kB2)};
-    while (true) {
+    // ~half of all x give a curve point; 128 failures (< 2^-128) never happen —
+    // the bound only guarantees termination.
+    for (int tries = 0; tries < 128; ++tries) {
         Fp2 x;
         x.c0 = rand_fq(rng);
         x.c1 = rand_fq(rng);
@@ -169,6 +175,7 @@ BD G2A hash_g2_from_seed(const uint8_t seed[32]) {
         const G2A h = g2_to_affine(g2_scale_by_cofactor(x, yy));
         if (!h.inf) return h;
     }
+    return {fp2_zero(), fp2_zero(), true};
 }
 
 // ------------------------------------------------------------------ G2Prepared
