@@ -574,6 +574,8 @@ BD bool g1_in_subgroup(const Fp& px, const Fp& py) {
 // zcash compressed G1 -> affine (Montgomery).  status: 0 ok, else invalid.
 BD bool g1_decompress(const uint8_t* b, G1A& out, bool check_subgroup) {
     const uint8_t f = b[0];
+    out.x = fp_zero();  // defined on every path (an undefined output lets the
+    out.y = fp_zero();  // optimiser drop the early-reject branches)
     out.inf = false;
     if (!(f & 0x80)) return false;
     if (f & 0x40) {  // infinity: everything else must be zero
@@ -693,6 +695,8 @@ BD bool g2_in_subgroup(const Fp2& qx, const Fp2& qy) {
 
 BD bool g2_decompress(const uint8_t* b, G2A& out, bool check_subgroup) {
     const uint8_t f = b[0];
+    out.x = fp2_zero();
+    out.y = fp2_zero();
     out.inf = false;
     if (!(f & 0x80)) return false;
     if (f & 0x40) {

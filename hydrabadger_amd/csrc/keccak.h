@@ -110,12 +110,21 @@ __device__ __forceinline__ void keccak_f(u64p (&a)[25]) {
     for (int r = 0; r < 24; ++r) keccak_round(a, kKeccakRC[2 * r], kKeccakRC[2 * r + 1]);
 }
 
+// IMPL 0: compiler-scheduled C round; 1: bank-allocated asm (keccak_asm.h)
+template <int IMPL>
+__device__ __forceinline__ void perm(u64p (&a)[25]);
+template <>
+__device__ __forceinline__ void perm<0>(u64p (&a)[25]) {
+    keccak_f(a);
+}
+
 __device__ __forceinline__ void keccak_zero(u64p (&a)[25]) {
 #pragma unroll
     for (int i = 0; i < 25; ++i) a[i] = {0u, 0u};
 }
 
 // SHA3-256 of a 64-byte message (left digest || right digest): hbbft hash_pair.
+template <int IMPL = 0>
 __device__ __forceinline__ void sha3_pair(const uint32_t (&l)[8], const uint32_t (&r)[8], uint32_t (&out)[8]) {
     u64p a[25];
     keccak_zero(a);
@@ -126,7 +135,7 @@ __device__ __forceinline__ void sha3_pair(const uint32_t (&l)[8], const uint32_t
     }
     a[8].lo = 0x06u;
     a[16].hi = 0x80000000u;
-    keccak_f(a);
+    perm<IMPL>(a);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         out[2 * i] = a[i].lo;
@@ -138,6 +147,7 @@ __device__ __forceinline__ void sha3_pair(const uint32_t (&l)[8], const uint32_t
 // bytes [0, round_up(len, 8)) — callers guarantee that range is mapped.
 // All lanes of a wave should pass the same `len` (the block loop is then
 // wave-uniform); `p` may differ per lane.
+template <int IMPL = 0>
 __device__ __forceinline__ void sha3_256_aligned8(const uint8_t* __restrict__ p, uint64_t len,
                                                   uint32_t (&out)[8]) {
     u64p a[25];
@@ -153,7 +163,7 @@ __device__ __forceinline__ void sha3_256_aligned8(const uint8_t* __restrict__ p,
             a[i].lo ^= w[i].x;
             a[i].hi ^= w[i].y;
         }
-        keccak_f(a);
+        perm<IMPL>(a);
         q += 17;
     }
     // final (possibly empty) block with FIPS-202 SHA3 padding
@@ -186,7 +196,7 @@ __device__ __forceinline__ void sha3_256_aligned8(const uint8_t* __restrict__ p,
         }
         a[16].hi ^= 0x80000000u;
     }
-    keccak_f(a);
+    perm<IMPL>(a);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         out[2 * i] = a[i].lo;

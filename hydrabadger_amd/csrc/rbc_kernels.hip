@@ -14,11 +14,13 @@
 //   shards + (k*N + i)*S,  S % 16 == 0,  L meaningful bytes, [L, S) scratch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <utility>
 
 #include "gf256.h"
 #include "keccak.h"
+#include "keccak_asm.h"
 #include "rbc_kernels.h"
 
 namespace hbg {
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
 // ============================================================== family 2: Merkle
 // One work-item per leaf; lanes_per_inst = next_pow2(N) (<= 256); tree levels
 // built in LDS by the owning lanes.  levels: [n][nodes][32].
+template <int IMPL>
 __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                     uint32_t N, uint32_t lpi, uint32_t nodes, uint64_t n,
                                                     uint8_t* __restrict__ levels) {
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
     uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)nodes * 32);
     if (live && leaf < N) {
         uint32_t d[8];
-        sha3_256_aligned8(shards + (inst * N + leaf) * S, L, d);
+        sha3_256_aligned8<IMPL>(shards + (inst * N + leaf) * S, L, d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) tree[leaf * 8 + i] = d[i];
         gout[2 * leaf] = make_uint4(d[0], d[1], d[2], d[3]);
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
                     l[i] = tree[(base + 2 * leaf) * 8 + i];
                     r[i] = tree[(base + 2 * leaf + 1) * 8 + i];
                 }
-                sha3_pair(l, r, d);
+                sha3_pair<IMPL>(l, r, d);
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) d[i] = tree[(base + 2 * leaf) * 8 + i];
@@ -309,6 +312,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
 }
 
 // Proof::validate(N) — one work-item per proof.
+template <int IMPL>
 __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len, const uint8_t* __restrict__ values,
                                                        uint64_t vstride, const uint32_t* __restrict__ index,
                                                        const uint8_t* __restrict__ digests, uint32_t depth,
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len,
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     uint32_t d[8];
-    sha3_256_aligned8(values + k * vstride, len, d);
+    sha3_256_aligned8<IMPL>(values + k * vstride, len, d);
     uint32_t li = index[k], ln = N, used = 0;
     const uint32_t nd = ndig[k];
     const uint32_t* dg = reinterpret_cast<const uint32_t*>(digests + k * (uint64_t)depth * 32);
@@ -333,8 +337,8 @@ __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len,
 #pragma unroll
             for (int i = 0; i < 8; ++i) s[i] = dg[used * 8 + i];
             ++used;
-            if (li & 1u) sha3_pair(s, d, d);
-            else sha3_pair(d, s, d);
+            if (li & 1u) sha3_pair<IMPL>(s, d, d);
+            else sha3_pair<IMPL>(d, s, d);
         }
         li >>= 1;
         ln = (ln + 1) >> 1;
@@ -439,6 +443,17 @@ __global__ __launch_bounds__(256) void synth_bytes(uint32_t tag, uint64_t first,
 }
 
 // ============================================================== launchers
+// Keccak implementation for the Merkle kernels: 1 = bank-allocated asm
+// (default), 0 = compiler-scheduled C round.  HBG_KECCAK_IMPL overrides (A/B
+// measurements only; both are bit-identical and covered by the parity tests).
+static int keccak_impl() {
+    static int v = [] {
+        const char* e = getenv("HBG_KECCAK_IMPL");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return v;
+}
+
 template <int D, int Q>
 static hipError_t launch_encode_const(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                       const uint8_t* payloads, uint64_t pstride, const uint64_t* plen,
@@ -498,7 +513,10 @@ hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, ui
     const uint32_t ipb = 256 / lpi;
     const uint64_t blocks = (n + ipb - 1) / ipb;
     const size_t lds = (size_t)ipb * nodes * 32;
-    merkle_build<<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
+    if (keccak_impl() == 1)
+        merkle_build<1><<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
+    else
+        merkle_build<0><<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
     return hipGetLastError();
 }
 
@@ -506,8 +524,12 @@ hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* value
                                   const uint32_t* index, const uint8_t* digests, uint32_t depth,
                                   const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
                                   hipStream_t st) {
-    merkle_validate<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index, digests,
-                                                                            depth, ndig, roots, ok, n);
+    if (keccak_impl() == 1)
+        merkle_validate<1><<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index,
+                                                                                   digests, depth, ndig, roots, ok, n);
+    else
+        merkle_validate<0><<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index,
+                                                                                   digests, depth, ndig, roots, ok, n);
     return hipGetLastError();
 }
 
