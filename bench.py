@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--instances", type=int, default=2048, help="1 MiB proposals per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="instances in the CPU-baseline sample")
+    ap.add_argument("--tdec-cts", type=int, default=1024,
+                    help="ciphertexts per TDec step (64 shares each, N=64 t=21); 0 disables the TDec leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     return ap.parse_args()
@@ -98,6 +100,120 @@ def cpu_baseline(n_sample: int):
             "sample": f"{n_sample} x 1 MiB send_shards (RS 22+42 AVX2 split-nibble + SHA3 Merkle), "
                       f"oracle/c/rbc_oracle.c -O3, one instance per thread, {dt:.2f} s wall",
             "simd": bool(corc.lib().orc_simd_enabled())}
+
+
+def _tdec_cpu_worker(args):
+    """One host process: verify `n` shares + `m` combines with the Python oracle."""
+    n, m = args
+    from oracle import bls12_381 as B
+    from oracle import tcrypto as T
+    g = _tdec_fixture()
+    cts = [T.Ciphertext(B.g1_decompress(bytes.fromhex(c["U"])), bytes.fromhex(c["V"]),
+                        B.g2_decompress(bytes.fromhex(c["W"]))) for c in g["cts"]]
+    pks = [B.g1_decompress(bytes.fromhex(p)) for p in g["pk_shares"]]
+    t0 = time.perf_counter()
+    good = 0
+    for k in range(n):
+        c = k % len(cts)
+        i = (k // len(cts)) % len(pks)
+        h = T.hash_g1_g2(cts[c].U, cts[c].V)  # per share: the crate recomputes it inside the call
+        good += T.verify_decryption_share(pks[i], B.g1_decompress(bytes.fromhex(g["cts"][c]["shares"][i])), cts[c], h)
+    t1 = time.perf_counter()
+    for k in range(m):
+        c = k % len(cts)
+        T.decrypt(g["t"], [(i, B.g1_decompress(bytes.fromhex(x))) for i, x in enumerate(g["cts"][c]["shares"])][
+            : g["t"] + 1], cts[c])
+    return t1 - t0, time.perf_counter() - t1, good
+
+
+def _tdec_fixture():
+    # N=64 t=21 key material (BASELINE.json configs[3]): 4 ciphertexts x 64 shares, made
+    # by tests/golden/make_golden_tdec.py.  Threshold material cannot be generated on the
+    # device yet (encrypt_with_rng is SURVEY.md §8(f1)); the fixture is replicated.
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "tdec_n64.json")))["scenario"]
+
+
+def cpu_baseline_tdec(per_proc: int = 6):
+    import multiprocessing as mp
+    procs = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    procs = max(1, min(procs, os.cpu_count() or 1, 16))
+    t0 = time.perf_counter()
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_tdec_cpu_worker, [(per_proc, 1)] * procs)
+    wall = time.perf_counter() - t0
+    tv = max(r[0] for r in res)
+    tc = max(r[1] for r in res)
+    return {"value": procs * per_proc / tv, "unit": "shares/s", "cores": procs, "kind": "port",
+            "combine_cts_per_s": procs / tc,
+            "sample": f"{procs} processes x {per_proc} verify_decryption_share + 1 decrypt (t=21), pure-Python "
+                      f"big-int oracle (oracle/tcrypto.py), {wall:.1f} s wall incl. process start",
+            "all_valid": all(r[2] == per_proc for r in res)}
+
+
+def tdec_leg(ctx, dev, n_ct: int, reps: int):
+    """Verify all 64 shares of n_ct ciphertexts (1 % corrupted) + combine the first
+    t+1 valid shares of each: hbg_tdec_verify_shares + hbg_tdec_combine on
+    device-resident inputs."""
+    from hydrabadger_amd import _lib
+    g = _tdec_fixture()
+    K, n, t = len(g["cts"]), len(g["pk_shares"]), g["t"]
+    base = [(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in g["cts"]]
+    U = np.frombuffer(b"".join(base[j % K][0] for j in range(n_ct)), np.uint8)
+    W = np.frombuffer(b"".join(base[j % K][2] for j in range(n_ct)), np.uint8)
+    Vb = b"".join(base[j % K][1] for j in range(n_ct))
+    off = np.zeros(n_ct + 1, np.uint64)
+    off[1:] = np.cumsum([len(base[j % K][1]) for j in range(n_ct)])
+    pk = np.frombuffer(b"".join(bytes.fromhex(p) for p in g["pk_shares"]), np.uint8)
+    sh_base = [[bytes.fromhex(x) for x in c["shares"]] for c in g["cts"]]
+    share = np.frombuffer(b"".join(sh_base[j % K][i] for j in range(n_ct) for i in range(n)), np.uint8)
+    sct = np.repeat(np.arange(n_ct, dtype=np.uint32), n)
+    spk = np.tile(np.arange(n, dtype=np.uint32), n_ct)
+    rng = np.random.default_rng(0x48424247)
+    bad = rng.random(n_ct * n) < 0.01          # seeded 1 % corrupted: claimed under the wrong key
+    spk[bad] = (spk[bad] + 1) % n
+    expect = (~bad).astype(np.uint8)
+    comb_sh, comb_ix = [], []
+    for j in range(n_ct):
+        good = [i for i in range(n) if not bad[j * n + i]][: t + 1]
+        comb_ix.append(good)
+        comb_sh.append(b"".join(sh_base[j % K][i] for i in good))
+    ix = np.array(comb_ix, np.uint32)
+    csh = np.frombuffer(b"".join(comb_sh), np.uint8)
+
+    def d(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dU, dW, dV, doff, dpk, dsh, dsct, dspk = (d(U), d(W), d(np.frombuffer(Vb, np.uint8)), d(off.view(np.int64)),
+                                              d(pk), d(share), d(sct.view(np.int32)), d(spk.view(np.int32)))
+    dix, dcsh = d(ix.view(np.int32)), d(csh)
+    ok = torch.empty(n_ct * n, dtype=torch.uint8, device=dev)
+    pt = torch.empty(max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
+    st = torch.empty(n_ct, dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
+
+    def verify():
+        _lib.check(L.hbg_tdec_verify_shares(ctx.h, n_ct, dU.data_ptr(), dV.data_ptr(), doff.data_ptr(),
+                                            dW.data_ptr(), n, dpk.data_ptr(), n_ct * n, dsh.data_ptr(),
+                                            dsct.data_ptr(), dspk.data_ptr(), ok.data_ptr(), flags), "verify")
+
+    def combine():
+        _lib.check(L.hbg_tdec_combine(ctx.h, t, n_ct, dcsh.data_ptr(), dix.data_ptr(), dV.data_ptr(),
+                                      doff.data_ptr(), pt.data_ptr(), st.data_ptr(), flags), "combine")
+    verify()
+    combine()
+    torch.cuda.synchronize()
+    bits_ok = bool(np.array_equal(ok.cpu().numpy(), expect))
+    ptb = pt.cpu().numpy().tobytes()
+    pts_ok = bool((st == 0).all().item()) and all(
+        ptb[int(off[j]):int(off[j + 1])] == bytes.fromhex(g["cts"][j % K]["plaintext"]) for j in range(n_ct))
+    ms_v = timed(verify, reps)
+    ms_c = timed(combine, reps)
+    return {"metric": "TDec shares/s (verify_decryption_share) at N=64 t=21", "unit": "shares/s",
+            "value": n_ct * n / ((ms_v + ms_c) * 1e-3), "verify_shares_per_s": n_ct * n / (ms_v * 1e-3),
+            "combine_cts_per_s": n_ct / (ms_c * 1e-3), "verify_ms": ms_v, "combine_ms": ms_c,
+            "n_ct": n_ct, "shares": n_ct * n, "corrupted": int(bad.sum()),
+            "ok_bits_match": bits_ok, "plaintexts_match": pts_ok,
+            "inputs": "tests/golden/tdec_n64.json (4 ciphertexts x 64 shares) replicated, HBM-resident"}
 
 
 def main():
@@ -200,9 +316,19 @@ def main():
         decode = {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
                   "erased_per_instance": parity, "roundtrip_ok": ok}
 
+    tdec = None
+    if a.tdec_cts > 0:
+        tdec = tdec_leg(ctx, dev, a.tdec_cts, max(2, min(a.steps, 5)))
+        if dist:
+            v = torch.tensor([tdec["value"]], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(v)  # whole-job shares/s (independent ciphertexts per rank)
+            tdec["value"] = float(v.item())
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_sample)
+        if tdec is not None:
+            tdec["cpu_baseline"] = cpu_baseline_tdec()
 
     if rank == 0:
         line = {
@@ -215,7 +341,7 @@ def main():
                        "parallelism": f"instances sharded over {world} GPU(s), no data-path collective"},
             "roofline": roofline, "kernels": kernels, "decode": decode, "cpu_baseline": cpu,
             "shard_bytes_GBps": value * N_NODES * L / PAYLOAD,
-            "tdec": None,
+            "tdec": tdec,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

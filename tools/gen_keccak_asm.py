@@ -45,7 +45,8 @@ class Alloc:
             i += 1
 
 
-def main():
+def layout():
+    """Returns (round body lines, A[x][y][h] register map, registers used)."""
     al = Alloc(0)
     # A[x][y][h]: bank (x + y) mod 4 — column triples y=0,1,2 distinct, y=3,4
     # distinct, partial-C bank free; spreads the state evenly over the banks
@@ -72,7 +73,7 @@ def main():
     taken = set()
     Cp = [[from_pool({(x + 1) % 4, (x + 2) % 4}, taken) for h in range(2)] for x in range(5)]  # partial C
     C = [[from_pool({0, 1, 2, 3}, taken) for h in range(2)] for x in range(5)]
-    T = [from_pool({0, 1, 2, 3}, taken), from_pool({0, 1, 2, 3}, taken)]
+    T = [[from_pool({0, 1, 2, 3}, taken), from_pool({0, 1, 2, 3}, taken)] for x in range(5)]
     D = Cp  # D is written after Cp is dead (no bank constraint on D)
     regs_used = sorted(al.used)
     nreg = max(regs_used) + 1
@@ -92,10 +93,10 @@ def main():
     for x in range(5):
         c1 = C[(x + 1) % 5]
         c0 = C[(x + 4) % 5]
-        L.append(f"v_alignbit_b32 {v(T[0])}, {v(c1[0])}, {v(c1[1])}, 31")
-        L.append(f"v_alignbit_b32 {v(T[1])}, {v(c1[1])}, {v(c1[0])}, 31")
-        L.append(f"v_xor_b32 {v(D[x][0])}, {v(c0[0])}, {v(T[0])}")
-        L.append(f"v_xor_b32 {v(D[x][1])}, {v(c0[1])}, {v(T[1])}")
+        L.append(f"v_alignbit_b32 {v(T[x][0])}, {v(c1[0])}, {v(c1[1])}, 31")
+        L.append(f"v_alignbit_b32 {v(T[x][1])}, {v(c1[1])}, {v(c1[0])}, 31")
+        L.append(f"v_xor_b32 {v(D[x][0])}, {v(c0[0])}, {v(T[x][0])}")
+        L.append(f"v_xor_b32 {v(D[x][1])}, {v(c0[1])}, {v(T[x][1])}")
     # theta apply + rho + pi
     for x in range(5):
         for y in range(5):
@@ -126,6 +127,80 @@ def main():
                 a, b, c = B[x][y][h], B[(x + 1) % 5][y][h], B[(x + 2) % 5][y][h]
                 # a ^ (~b & c): truth table over (S0=a, S1=b, S2=c) with index (a<<2)|(b<<1)|c
                 L.append(f"v_bitop3_b32 {v(A[x][y][h])}, {v(a)}, {v(b)}, {v(c)} bitop3:0xd2")
+    return L, A, sorted(al.used)
+
+
+def _parse(line):
+    op, rest = line.split(None, 1)
+    regs = [t.strip() for t in rest.split(" bitop3")[0].split(",")]
+    regs = [int(t[1:]) for t in regs if t.startswith("v")]
+    return op, regs[0], regs[1:]
+
+
+def schedule(lines, lat=2, gap=2):
+    """Greedy list schedule of one round: spreads the half-rate v_alignbit ops
+    between full-rate ops (at most one alignbit per `gap` full-rate ops when
+    both are ready) and keeps `lat` slots between a producer and its consumer
+    where possible; ties broken by critical-path length.  Register RAW/WAR/WAW
+    dependencies are preserved exactly."""
+    n = len(lines)
+    info = [_parse(x) for x in lines]
+    preds = [set() for _ in range(n)]
+    raw = [set() for _ in range(n)]
+    last_w, readers = {}, {}
+    for i, (op, d, srcs) in enumerate(info):
+        for r in srcs:
+            if r in last_w:
+                preds[i].add(last_w[r])
+                raw[i].add(last_w[r])
+        for j in readers.get(d, []):
+            if j != i:
+                preds[i].add(j)
+        if d in last_w:
+            preds[i].add(last_w[d])
+        for r in srcs:
+            readers.setdefault(r, []).append(i)
+        last_w[d] = i
+        readers[d] = []
+    succs = [[] for _ in range(n)]
+    for i in range(n):
+        for j in preds[i]:
+            succs[j].append(i)
+    half = [info[i][0] == "v_alignbit_b32" for i in range(n)]
+    cp = [0] * n
+    for i in reversed(range(n)):
+        w = 2 if half[i] else 1
+        cp[i] = w + max((cp[j] for j in succs[i]), default=0)
+    done_at = {}
+    out = []
+    since_half = gap
+    remaining = set(range(n))
+    t = 0
+    while remaining:
+        ready = [i for i in remaining if all(p in done_at for p in preds[i])]
+        def key(i):
+            stall = any(t - done_at[p] < lat for p in raw[i])
+            want_half = since_half >= gap
+            cls = 0 if half[i] == want_half else 1
+            return (stall, cls, -cp[i], i)
+        i = min(ready, key=key)
+        out.append(lines[i])
+        done_at[i] = t
+        remaining.discard(i)
+        since_half = 0 if half[i] else since_half + 1
+        t += 1
+    return out
+
+
+def main():
+    L, A, regs_used = layout()
+    if os.environ.get("KECCAK_SCHED", "1") == "1":
+        L = schedule(L)
+    nreg = max(regs_used) + 1
+
+    def v(i):
+        return f"v{i}"
+
     # iota: RC from the scalar table, loop control
     body = "\\n\\t".join(L)
     asm_lines = [

@@ -49,6 +49,11 @@ def main():
             d["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / max(m["SQ_WAVES"], 1)
         if "SQ_ACTIVE_INST_VALU" in m and "SQ_BUSY_CYCLES" in m:
             d["valu_active_per_busy"] = m["SQ_ACTIVE_INST_VALU"] / max(m["SQ_BUSY_CYCLES"], 1)
+        if "GRBM_GUI_ACTIVE" in m and dur.get(k):
+            # summed over the 8 XCDs (MI355X_MICROARCH.md 'DVFS give-back')
+            ms = sum(dur[k]) / len(dur[k])
+            d["avg_ms"] = ms
+            d["effective_clock_GHz"] = m["GRBM_GUI_ACTIVE"] / 8 / (ms * 1e-3) / 1e9
         if "FETCH_SIZE" in m:
             d["hbm_read_bytes_corrected"] = m["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in m:
