@@ -226,7 +226,7 @@ def main():
     if dist:
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from hydrabadger_amd import _lib
+    from hydrabadger_amd import _lib, shard
     from hydrabadger_amd import broadcast as bc
 
     dev = torch.device("cuda", local)
@@ -240,7 +240,7 @@ def main():
     S = (L + 15) // 16 * 16
     nodes = _lib.merkle_nodes(N_NODES)
     data, parity = bc.shard_counts(N_NODES)
-    first = rank * B
+    first = shard.instance_block(rank, world, B).start
     pay = torch.empty((B, PAYLOAD), dtype=torch.uint8, device=dev)
     bc.synth_bytes(1, first, PAYLOAD, pay, ctx=ctx, device=True)
     plen = torch.full((B,), PAYLOAD, dtype=torch.int64, device=dev)
@@ -262,11 +262,7 @@ def main():
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
-    dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = shard.max_over_ranks(time.perf_counter() - t0, dev)
     total_bytes = world * B * PAYLOAD * a.steps
     value = total_bytes / dt / 1e9
 
@@ -319,10 +315,7 @@ def main():
     tdec = None
     if a.tdec_cts > 0:
         tdec = tdec_leg(ctx, dev, a.tdec_cts, max(2, min(a.steps, 5)))
-        if dist:
-            v = torch.tensor([tdec["value"]], dtype=torch.float64, device=dev)
-            torch.distributed.all_reduce(v)  # whole-job shares/s (independent ciphertexts per rank)
-            tdec["value"] = float(v.item())
+        tdec["value"] = shard.sum_over_ranks(tdec["value"], dev)  # whole-job shares/s
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
