@@ -156,6 +156,66 @@ __device__ __forceinline__ uint32_t cmul_acc(uint32_t acc, const Pow8& P) {
     return acc;
 }
 
+// ------------------------------------------------------------- split-nibble form
+// c*w = Lo[c & 15] ^ Hi[c >> 4] with Lo[m] = XOR_{i in m} alpha^i w and
+// Hi[m] = XOR_{i in m} alpha^(4+i) w (the GPU analogue of rse's PSHUFB
+// low/high nibble tables, but over the 8 SWAR powers of one data word).
+// xtime via v_perm: the reduction byte (0x1D or 0) is selected by each
+// byte's top bit, so one xtime = lshr, and, perm, lshl, bitop3.
+__device__ __forceinline__ uint32_t xtime4p(uint32_t w) {
+    const uint32_t sel = (w >> 7) & 0x01010101u;               // 0/1 per byte
+    const uint32_t red = __builtin_amdgcn_perm(0u, 0x00001D00u, sel);  // byte -> 0x00 / 0x1D
+    return __builtin_amdgcn_bitop3_b32(w << 1, 0xFEFEFEFEu, red, 0x6A);  // (a & b) ^ c
+}
+
+// One nibble table: T[m] for m in 1..15 from the four powers q0..q3 (T[0] unused).
+// Entries are computed lazily by the compiler: only those a column's
+// compile-time coefficients reference survive dead-code elimination.
+struct NibTab {
+    uint32_t t[16];
+};
+
+__device__ __forceinline__ NibTab nib_table(uint32_t q0, uint32_t q1, uint32_t q2, uint32_t q3) {
+    NibTab r;
+    r.t[0] = 0u;
+    r.t[1] = q0;
+    r.t[2] = q1;
+    r.t[4] = q2;
+    r.t[8] = q3;
+    r.t[3] = q0 ^ q1;
+    r.t[5] = q0 ^ q2;
+    r.t[6] = q1 ^ q2;
+    r.t[9] = q0 ^ q3;
+    r.t[10] = q1 ^ q3;
+    r.t[12] = q2 ^ q3;
+    r.t[7] = xor3u(q0, q1, q2);
+    r.t[11] = xor3u(q0, q1, q3);
+    r.t[13] = xor3u(q0, q2, q3);
+    r.t[14] = xor3u(q1, q2, q3);
+    r.t[15] = r.t[3] ^ r.t[12];
+    return r;
+}
+
+struct NibPair {
+    NibTab lo, hi;
+};
+
+__device__ __forceinline__ NibPair nib_tables(uint32_t w) {
+    const uint32_t p1 = xtime4p(w), p2 = xtime4p(p1), p3 = xtime4p(p2), p4 = xtime4p(p3);
+    const uint32_t p5 = xtime4p(p4), p6 = xtime4p(p5), p7 = xtime4p(p6);
+    return {nib_table(w, p1, p2, p3), nib_table(p4, p5, p6, p7)};
+}
+
+// acc ^ (C * w) for a compile-time coefficient: one bitop3 (or xor) per pair.
+template <uint8_t C>
+__device__ __forceinline__ uint32_t nib_mac(uint32_t acc, const NibPair& T) {
+    constexpr int lo = C & 15, hi = C >> 4;
+    if constexpr (lo && hi) return xor3u(acc, T.lo.t[lo], T.hi.t[hi]);
+    else if constexpr (lo) return acc ^ T.lo.t[lo];
+    else if constexpr (hi) return acc ^ T.hi.t[hi];
+    else return acc;
+}
+
 // c * w for a run-time (wave-uniform) coefficient.
 __device__ __forceinline__ uint32_t rmul(uint32_t c, const Pow8& P) {
     uint32_t r = 0;

@@ -49,55 +49,126 @@ __device__ __forceinline__ uint32_t value_word(const uint8_t* __restrict__ pay, 
 }
 
 template <int D, int Q, int J, int... K>
-__device__ __forceinline__ void mac_column(uint32_t (&acc)[Q], const Pow8& P, std::integer_sequence<int, K...>) {
-    ((acc[K] = cmul_acc<kParity<D, Q>.m[K][J]>(acc[K], P)), ...);
+__device__ __forceinline__ void mac_column(uint32_t (&acc)[Q], const NibPair& T, std::integer_sequence<int, K...>) {
+    ((acc[K] = nib_mac<kParity<D, Q>.m[K][J]>(acc[K], T)), ...);
 }
 
-template <int D, int Q, bool FROM_PAYLOAD, int J>
-__device__ __forceinline__ void encode_column(uint32_t (&acc)[Q], uint8_t* __restrict__ inst_base, uint64_t S,
-                                              uint64_t L, uint32_t p, const uint8_t* __restrict__ pay,
-                                              uint64_t P) {
-    uint32_t* row = reinterpret_cast<uint32_t*>(inst_base + (uint64_t)J * S);
-    uint32_t w;
-    if constexpr (FROM_PAYLOAD) {
-        w = value_word(pay, P, (uint64_t)J * L + 4 * (uint64_t)p);
-        row[p] = w;
-    } else {
-        w = row[p];
+// Data words: MODE 0 rows already in place (Coding::encode); 1 from the
+// payload, edge-checked (send_shards' prefix, padding, last partial word);
+// 2 from the payload, interior block — every row's word lies inside the
+// payload, so the address is a wave-uniform row base + p and the byte shift
+// (J*L mod 4) is uniform: one dwordx2 load + v_alignbyte per word, no
+// per-lane branches.  Loads run kPrefetch columns ahead of the arithmetic.
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+constexpr int kPrefetch = 6;
+
+template <int D, int Q, int MODE>
+struct EncodeCtx {
+    uint8_t* __restrict__ base;
+    uint64_t S, L;
+    uint32_t p;
+    const uint8_t* __restrict__ pay;
+    uint64_t P;
+    u32x2_a4 buf[kPrefetch];
+
+    template <int J>
+    __device__ __forceinline__ void fetch() {
+        if constexpr (J < D) {
+            if constexpr (MODE == 2) {
+                const uint64_t o = (uint64_t)J * L + 4 * (uint64_t)p - 4;  // payload byte of value byte J*L + 4p
+                buf[J % kPrefetch] = *reinterpret_cast<const u32x2_a4*>(pay + (o & ~3ull));
+            } else if constexpr (MODE == 0) {
+                buf[J % kPrefetch].x = reinterpret_cast<const uint32_t*>(base + (uint64_t)J * S)[p];
+            }
+        }
     }
-    const Pow8 pw = powers(w);
-    mac_column<D, Q, J>(acc, pw, std::make_integer_sequence<int, Q>{});
+
+    template <int J>
+    __device__ __forceinline__ uint32_t word() {
+        uint32_t* row = reinterpret_cast<uint32_t*>(base + (uint64_t)J * S);
+        uint32_t w;
+        if constexpr (MODE == 2) {
+            const uint64_t o = (uint64_t)J * L + 4 * (uint64_t)p - 4;
+            w = __builtin_amdgcn_alignbyte(buf[J % kPrefetch].y, buf[J % kPrefetch].x, (uint32_t)(o & 3));
+            row[p] = w;
+        } else if constexpr (MODE == 1) {
+            w = value_word(pay, P, (uint64_t)J * L + 4 * (uint64_t)p);
+            row[p] = w;
+        } else {
+            w = buf[J % kPrefetch].x;
+        }
+        return w;
+    }
+
+    template <int J>
+    __device__ __forceinline__ void column(uint32_t (&acc)[Q]) {
+        fetch<J + kPrefetch - 1>();
+        uint32_t w = word<J>();
+        // Column sequencing: the volatile (mutually ordered) empty asms pin this
+        // column's tables after the previous column's accumulators, so only one
+        // column's 30 table VGPRs are live; they also fence memory ops, which is
+        // why the loads are issued explicitly kPrefetch-1 columns ahead above.
+        asm volatile("" : "+v"(w));
+        const NibPair T = nib_tables(w);
+        mac_column<D, Q, J>(acc, T, std::make_integer_sequence<int, Q>{});
+#pragma unroll
+        for (int k = 0; k < Q; ++k) asm volatile("" : "+v"(acc[k]));
+    }
+
+    template <int... J>
+    __device__ __forceinline__ void prologue(std::integer_sequence<int, J...>) {
+        (fetch<J>(), ...);
+    }
+    template <int... J>
+    __device__ __forceinline__ void columns(uint32_t (&acc)[Q], std::integer_sequence<int, J...>) {
+        (column<J>(acc), ...);
+    }
+};
+
+template <int D, int Q, int MODE>
+__device__ __forceinline__ void encode_word(uint8_t* __restrict__ base, uint64_t S, uint64_t L, uint32_t p,
+                                            const uint8_t* __restrict__ pay, uint64_t P) {
+    EncodeCtx<D, Q, MODE> cx{base, S, L, p, pay, P, {}};
+    uint32_t acc[Q];
+#pragma unroll
+    for (int k = 0; k < Q; ++k) acc[k] = 0u;
+    cx.prologue(std::make_integer_sequence<int, kPrefetch - 1>{});
+    cx.columns(acc, std::make_integer_sequence<int, D>{});
+#pragma unroll
+    for (int k = 0; k < Q; ++k) reinterpret_cast<uint32_t*>(base + (uint64_t)(D + k) * S)[p] = acc[k];
 }
 
-template <int D, int Q, bool FROM_PAYLOAD, int... J>
-__device__ __forceinline__ void encode_all(uint32_t (&acc)[Q], uint8_t* __restrict__ inst_base, uint64_t S,
-                                           uint64_t L, uint32_t p, const uint8_t* __restrict__ pay, uint64_t P,
-                                           std::integer_sequence<int, J...>) {
-    (encode_column<D, Q, FROM_PAYLOAD, J>(acc, inst_base, S, L, p, pay, P), ...);
-}
-
-// One thread = 4 byte positions of one instance, all N shards.
+// One thread = 4 byte positions of one instance, all N shards; one 256-thread
+// block = 1 KiB of every row.  The coding matrix is compile-time, so every
+// GF(2^8) product is a split-nibble table lookup resolved at compile time
+// (one v_bitop3 per (parity row, data row) pair).
 template <int D, int Q, bool FROM_PAYLOAD>
-__global__ __launch_bounds__(256) void rs_encode_const(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+__global__ __launch_bounds__(256, 4) void rs_encode_const(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                        uint64_t n, uint32_t blocks_per_inst,
                                                        const uint8_t* __restrict__ payloads, uint64_t pstride,
                                                        const uint64_t* __restrict__ plen) {
     const uint64_t inst = blockIdx.x / blocks_per_inst;
-    const uint32_t p = (blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
-    if (inst >= n || 4 * (uint64_t)p >= L) return;
+    const uint32_t blk = blockIdx.x % blocks_per_inst;
+    const uint32_t p = blk * 256 + threadIdx.x;
+    if (inst >= n) return;
     uint8_t* base = shards + inst * (uint64_t)(D + Q) * S;
-    const uint8_t* pay = nullptr;
-    uint64_t P = 0;
     if constexpr (FROM_PAYLOAD) {
-        pay = payloads + inst * pstride;
-        P = plen[inst];
+        const uint8_t* pay = payloads + inst * pstride;
+        const uint64_t P = plen[inst];
+        const uint64_t end = 4 * (uint64_t)(blk * 256 + 256);  // value-byte end of this block in a row
+        // interior: past the length prefix, inside the row, and the last row's
+        // dwordx2 window [.., (D-1)L + end + 4) inside the payload (+4 prefix)
+        const bool interior = blk > 0 && end <= L && (uint64_t)(D - 1) * L + end + 4 <= P + 4;
+        if (interior) {
+            encode_word<D, Q, 2>(base, S, L, p, pay, P);
+        } else {
+            if (4 * (uint64_t)p >= L) return;
+            encode_word<D, Q, 1>(base, S, L, p, pay, P);
+        }
+    } else {
+        if (4 * (uint64_t)p >= L) return;
+        encode_word<D, Q, 0>(base, S, L, p, nullptr, 0);
     }
-    uint32_t acc[Q];
-#pragma unroll
-    for (int k = 0; k < Q; ++k) acc[k] = 0u;
-    encode_all<D, Q, FROM_PAYLOAD>(acc, base, S, L, p, pay, P, std::make_integer_sequence<int, D>{});
-#pragma unroll
-    for (int k = 0; k < Q; ++k) reinterpret_cast<uint32_t*>(base + (uint64_t)(D + k) * S)[p] = acc[k];
 }
 
 // Pack only (Trivial coding, N <= 3): send_shards' buffer into N rows.

@@ -7,6 +7,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# torch bundles its own libamdhip64.so.7 (same soname as /opt/rocm's): load it
+# before libhbgpu.so so the whole test process runs on ONE HIP runtime, as
+# bench.py does (torch first).  Loading libhbgpu.so first made torch's CUDA
+# unavailable and silently skipped the device-resident (torch) tests.
+try:
+    import torch  # noqa: F401
+except ImportError:  # CPU-only environments without torch still run the oracle tests
+    torch = None
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libhbgpu.so on the device)")

@@ -309,3 +309,38 @@ def test_device_roundtrip_erase_decode(N, P, n):
     torch.cuda.synchronize()
     s = st.cpu().tolist()
     assert s[1] == 0 and all(v == 1 for i, v in enumerate(s) if i != 1)
+
+
+def test_device_batch_mixed_payload_lengths():
+    """Per-instance payload lengths that share one shard length L (the batch
+    contract): exercises the encoder's interior/edge block split at every
+    tail position (last-row padding boundary moves with P)."""
+    torch = _torch()
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    N = 64
+    D, _ = bc.shard_counts(N)
+    P0 = 1 << 20
+    L = _lib.shard_len(N, P0)
+    lens = [D * L - 4, D * L - 5, D * (L - 1) - 3, P0, P0 - 1, P0 - 9, D * (L - 1) - 2]
+    assert all(_lib.shard_len(N, p) == L for p in lens)
+    n = len(lens)
+    S = (L + 15) // 16 * 16
+    dev = torch.device("cuda:0")
+    PS = (max(lens) + 15) // 16 * 16
+    pays = [np.frombuffer(synth.payload(1300 + k, p), np.uint8) for k, p in enumerate(lens)]
+    host = np.zeros((n, PS), np.uint8)
+    for k, p in enumerate(pays):
+        host[k, :len(p)] = p
+    pay = torch.from_numpy(host).to(dev)
+    plen = torch.tensor(lens, dtype=torch.int64, device=dev)
+    shards = torch.empty((n, N, S), dtype=torch.uint8, device=dev)
+    levels = torch.empty((n, _lib.merkle_nodes(N), 32), dtype=torch.uint8, device=dev)
+    bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels, device=True)
+    torch.cuda.synchronize()
+    sh = shards.cpu().numpy()
+    lv = levels.cpu().numpy()
+    for k in range(n):
+        rs, rl = corc.rbc_encode_merkle(N, pays[k].copy())
+        assert np.array_equal(sh[k, :, :L], rs), k
+        assert np.array_equal(lv[k], rl), k
