@@ -64,9 +64,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--instances", type=int, default=2048, help="1 MiB proposals per GPU per step")
+    ap.add_argument("--instances", type=int, default=8192, help="1 MiB proposals per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="instances in the CPU-baseline sample")
-    ap.add_argument("--tdec-cts", type=int, default=1024,
+    ap.add_argument("--tdec-cts", type=int, default=16384,
                     help="ciphertexts per TDec step (64 shares each, N=64 t=21); 0 disables the TDec leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
