@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1024, help="instances in the CPU-baseline sample")
     ap.add_argument("--tdec-cts", type=int, default=16384,
                     help="ciphertexts per TDec step (64 shares each, N=64 t=21); 0 disables the TDec leg")
+    ap.add_argument("--epoch-nodes", type=int, default=128,
+                    help="configs[4]: one N-node network spanning all ranks (RCCL all-gather); 0 disables")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     return ap.parse_args()
@@ -216,6 +218,38 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int):
             "inputs": "tests/golden/tdec_n64.json (4 ciphertexts x 64 shares) replicated, HBM-resident"}
 
 
+def network_leg(ctx, dev, n_nodes: int, reps: int):
+    """configs[4]: the RBC half of one epoch of ONE n_nodes-node network whose
+    nodes are split over all ranks (hydrabadger_amd/network.py): encode the
+    local proposals, one all-gather of shards + Merkle levels (RCCL over xGMI),
+    validate every echo proof, decode all n_nodes proposals.  Timed per phase
+    on every rank, max over ranks."""
+    from hydrabadger_amd import network, shard
+    eng = network.DeviceEngine(dev, ctx)
+    ep = network.SpanningEpoch(n_nodes, PAYLOAD, eng)
+    pay = eng.synth_payloads(ep.rank * ep.m, ep.m, PAYLOAD)
+    res = ep.run(pay)  # warm
+    ok = bool((res.status == 1).all().item()) and bool(res.echo_ok.all().item())
+    own = res.payloads[ep.rank * ep.m:(ep.rank + 1) * ep.m, :PAYLOAD]
+    ok = ok and bool(torch.equal(own, pay[:, :PAYLOAD]))
+    phases = {}
+    for _ in range(reps):
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        r = ep.run(pay)
+        for k, v in r.times_ms.items():
+            phases[k] = phases.get(k, 0.0) + v / reps
+    phases = {k: shard.max_over_ranks(v, dev) for k, v in phases.items()}
+    recv = res.exchange_bytes
+    return {"workload": f"one {n_nodes}-node network (RS {ep.N - 2 * ((ep.N - 1) // 3)}+{2 * ((ep.N - 1) // 3)}), "
+                        f"1 MiB proposals, nodes split over {ep.world} rank(s)",
+            "nodes_per_rank": ep.m, "epoch_ms": phases["epoch"], "phases_ms": phases,
+            "proposals_per_s": n_nodes / (phases["epoch"] * 1e-3),
+            "allgather_recv_bytes_per_rank": recv,
+            "allgather_GBps": (recv / (phases["all_gather"] * 1e-3) / 1e9) if recv else None,
+            "all_decoded_ok": ok}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -312,6 +346,10 @@ def main():
         decode = {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
                   "erased_per_instance": parity, "roundtrip_ok": ok}
 
+    epoch = None
+    if a.epoch_nodes > 0 and a.epoch_nodes % world == 0:
+        epoch = network_leg(ctx, dev, a.epoch_nodes, max(2, min(a.steps, 5)))
+
     tdec = None
     if a.tdec_cts > 0:
         tdec = tdec_leg(ctx, dev, a.tdec_cts, max(2, min(a.steps, 5)))
@@ -335,6 +373,7 @@ def main():
             "roofline": roofline, "kernels": kernels, "decode": decode, "cpu_baseline": cpu,
             "shard_bytes_GBps": value * N_NODES * L / PAYLOAD,
             "tdec": tdec,
+            "network_epoch": epoch,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
