@@ -326,7 +326,7 @@ def main():
     decode = None
     if not a.no_decode:
         from hydrabadger_amd import workload
-        nd = min(B, 512)
+        nd = min(B, 2048)
         present = torch.tensor([workload.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
                                dtype=torch.uint8, device=dev)
         roots = levels[:nd, nodes - 1, :].contiguous()

@@ -133,6 +133,14 @@ int device_encode_plan(hbg_ctx* c, uint32_t D, uint32_t Q, uint8_t** out) {
     for (uint32_t j = 0; j < D; ++j) p->in_idx[j] = (uint8_t)j;
     for (uint32_t k = 0; k < Q; ++k) p->out_idx[k] = (uint8_t)(D + k);
     memcpy(h.data() + sizeof(CodePlan), m.data() + (size_t)D * D, (size_t)Q * D);
+    uint32_t* offs = reinterpret_cast<uint32_t*>(h.data() + plan_offs_at(D, Q));
+    const uint32_t qp = plan_qpad(Q);
+    for (uint32_t j = 0; j < D; ++j)
+        for (uint32_t k = 0; k < qp; ++k) {
+            const uint8_t cf = k < Q ? m[(size_t)(D + k) * D + j] : 0;
+            offs[2 * ((size_t)j * qp + k)] = nib_off_lo(cf);
+            offs[2 * ((size_t)j * qp + k) + 1] = nib_off_hi(cf);
+        }
     uint8_t* d = nullptr;
     if (hipMalloc(&d, ps) != hipSuccess) return HBG_E_NOMEM;
     HBG_TRY(hipMemcpy(d, h.data(), ps, hipMemcpyHostToDevice));

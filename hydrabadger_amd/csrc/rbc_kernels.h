@@ -10,7 +10,11 @@ namespace hbg {
 
 // Per-instance coding plan consumed by rs_code_generic:
 // out_row[out_idx[o]] = XOR_j coef[o][j] * row[in_idx[j]],  coef follows the
-// struct as [n_out][D] bytes.
+// struct as [n_out][D] bytes; then (16-B aligned, plan_offs_at) the same
+// coefficients as split-nibble LDS byte offsets, u32 [D][plan_qpad][2] =
+// {(c & 15) * 256, (16 + (c >> 4)) * 256} — read by scalar loads; rows
+// o >= n_out are {0, 16 * 256} (the zero entries), so whole output tiles
+// run unguarded.
 struct CodePlan {
     int32_t status;  // 0 or HBG_E_*
     uint32_t n_out;
@@ -36,8 +40,20 @@ __host__ __device__ constexpr uint32_t merkle_depth(uint32_t n) {
     return d;
 }
 
-inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
+__host__ __device__ constexpr uint64_t plan_offs_at(uint32_t D, uint32_t max_out) {
     return (sizeof(CodePlan) + (uint64_t)max_out * D + 15) & ~uint64_t(15);
+}
+
+__host__ __device__ constexpr uint32_t nib_off_lo(uint32_t c) { return (c & 15u) * 256u; }
+__host__ __device__ constexpr uint32_t nib_off_hi(uint32_t c) { return (16u + (c >> 4)) * 256u; }
+
+constexpr uint32_t kGenericTile = 48;  // output rows per rs_code_generic register tile
+__host__ __device__ constexpr uint32_t plan_qpad(uint32_t max_out) {
+    return (max_out + kGenericTile - 1) / kGenericTile * kGenericTile;
+}
+
+inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
+    return plan_offs_at(D, max_out) + 8ull * D * plan_qpad(max_out);
 }
 
 bool has_const_encoder(uint32_t D, uint32_t Q);

@@ -186,37 +186,62 @@ __global__ __launch_bounds__(256) void pack_rows(uint8_t* __restrict__ shards, u
 }
 
 // Generic coding: out_row[o] = XOR_j coef[o][j] * in_row[j] for one instance's
-// plan (see rbc_kernels.h CodePlan).  Output tile of 32 rows in registers.
-constexpr int kGenericTile = 32;
+// plan (see rbc_kernels.h CodePlan) — reconstruct (per-instance coefficients)
+// and encode for (D, Q) without a compile-time encoder.  Coefficients are
+// run-time but wave-uniform, so the split-nibble tables of each input word
+// go to LDS (lane-private slots, [wave][32 entries][64 lanes]: conflict-free)
+// and every (output, input) pair is two LDS lookups + one v_bitop3.  Output
+// rows are tiled kGenericTile at a time in registers.
+constexpr uint32_t kGenericLds = 4 * 32 * 64 * 4;  // 32 KiB per 256-thread block
 
 __global__ __launch_bounds__(256) void rs_code_generic(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                        uint32_t N, uint32_t D, uint64_t n,
                                                        uint32_t blocks_per_inst, const uint8_t* __restrict__ plans,
                                                        uint64_t plan_stride) {
+    extern __shared__ uint32_t gtab[];
+    typedef const __attribute__((address_space(4))) uint32_t* cu32;  // scalar (SMEM) loads
     const uint64_t inst = blockIdx.x / blocks_per_inst;
     const uint32_t p = (blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
     if (inst >= n) return;
-    const CodePlan* plan = reinterpret_cast<const CodePlan*>(plans + inst * plan_stride);
-    if (plan->status != 0 || 4 * (uint64_t)p >= L) return;
+    const uint32_t Q = N - D, qp = plan_qpad(Q);
+    const uint8_t* pbase = plans + inst * plan_stride;
+    const CodePlan* plan = reinterpret_cast<const CodePlan*>(pbase);
+    if (plan->status != 0) return;
     const uint32_t n_out = plan->n_out;
-    const uint8_t* coef = reinterpret_cast<const uint8_t*>(plan) + sizeof(CodePlan);
+    const bool active = 4 * (uint64_t)p < L;
+    const cu32 offs = (cu32)(pbase + plan_offs_at(D, Q));
     uint8_t* base = shards + inst * (uint64_t)N * S;
+    uint32_t* tab = gtab + (threadIdx.x >> 6) * (32 * 64) + (threadIdx.x & 63);  // entry e at tab[64 e]
+    const uint32_t tab_addr = (uint32_t)(uintptr_t)tab;                             // LDS byte address
+    tab[0] = 0u;
+    tab[16 * 64] = 0u;
     for (uint32_t o0 = 0; o0 < n_out; o0 += kGenericTile) {
         uint32_t acc[kGenericTile];
 #pragma unroll
-        for (int o = 0; o < kGenericTile; ++o) acc[o] = 0u;
+        for (int o = 0; o < (int)kGenericTile; ++o) acc[o] = 0u;
         const uint32_t cnt = (n_out - o0) < (uint32_t)kGenericTile ? (n_out - o0) : (uint32_t)kGenericTile;
         for (uint32_t j = 0; j < D; ++j) {
-            const uint32_t w = reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p];
-            const Pow8 pw = powers(w);
+            const uint32_t w =
+                active ? reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p] : 0u;
+            const NibPair T = nib_tables(w);
 #pragma unroll
-            for (int o = 0; o < kGenericTile; ++o)
-                if ((uint32_t)o < cnt) acc[o] ^= rmul(coef[(o0 + o) * D + j], pw);
+            for (int e = 1; e < 16; ++e) {
+                tab[64 * e] = T.lo.t[e];
+                tab[64 * (16 + e)] = T.hi.t[e];
+            }
+            const cu32 oj = offs + 2 * ((uint64_t)j * qp + o0);
+            typedef const __attribute__((address_space(3))) uint32_t* lds32;
+#pragma unroll
+            for (int o = 0; o < (int)kGenericTile; ++o)  // rows >= cnt read the zero entries
+                acc[o] = xor3u(acc[o], *(lds32)(uintptr_t)(tab_addr + oj[2 * o]),
+                               *(lds32)(uintptr_t)(tab_addr + oj[2 * o + 1]));
         }
+        if (active) {
 #pragma unroll
-        for (int o = 0; o < kGenericTile; ++o)
-            if ((uint32_t)o < cnt)
-                reinterpret_cast<uint32_t*>(base + (uint64_t)plan->out_idx[o0 + o] * S)[p] = acc[o];
+            for (int o = 0; o < (int)kGenericTile; ++o)
+                if ((uint32_t)o < cnt)
+                    reinterpret_cast<uint32_t*>(base + (uint64_t)plan->out_idx[o0 + o] * S)[p] = acc[o];
+        }
     }
 }
 
@@ -242,6 +267,8 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
     const uint8_t* pr = present + inst * N;
     CodePlan* plan = reinterpret_cast<CodePlan*>(plans + inst * plan_stride);
     uint8_t* coef = reinterpret_cast<uint8_t*>(plan) + sizeof(CodePlan);
+    uint32_t* offs = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(plan) + plan_offs_at(D, Q));
+    const uint32_t qp = plan_qpad(Q);
     const uint32_t t = threadIdx.x;
     // GF tables into LDS
     for (uint32_t i = t; i < 256; i += blockDim.x) lg[i] = kGf.log[i];
@@ -321,6 +348,13 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
         uint32_t acc = 0;
         for (uint32_t k = 0; k < D; ++k) acc ^= gmul(mrow[k], aug[k * W + D + c]);
         coef[o * D + c] = (uint8_t)acc;
+        offs[2 * (c * qp + o)] = nib_off_lo(acc);
+        offs[2 * (c * qp + o) + 1] = nib_off_hi(acc);
+    }
+    for (uint32_t e = t; e < (qp - no) * D; e += blockDim.x) {  // padding rows: the zero entries
+        const uint32_t o = no + e / D, c = e % D;
+        offs[2 * (c * qp + o)] = nib_off_lo(0);
+        offs[2 * (c * qp + o) + 1] = nib_off_hi(0);
     }
     for (uint32_t j = t; j < D; j += blockDim.x) plan->in_idx[j] = (uint8_t)s_rows[j];
     for (uint32_t o = t; o < no; o += blockDim.x) plan->out_idx[o] = s_out[o];
@@ -564,7 +598,7 @@ hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N,
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
-    rs_code_generic<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, D, n, bpi, plans,
+    rs_code_generic<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
                                                                       plan_stride);
     return hipGetLastError();
 }
