@@ -6,6 +6,8 @@
 // calls (HBG_DEVICE) run in place on the caller's buffers.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -23,7 +25,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 16;
+constexpr int kNumSlots = 32;
 
 struct Buf {
     void* p = nullptr;
@@ -39,6 +41,7 @@ struct hbg_ctx {
     Buf slot[kNumSlots];
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> matrices;  // device (D+Q) x D coding matrices
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> enc_plans; // device shared encode plans
+    int tdec_batched = 1;  // batched share verification (hbg_test_set_tdec_batched / HBG_TDEC_BATCHED=0)
     std::mutex mu;
 };
 
@@ -242,6 +245,7 @@ int hbg_init(hbg_ctx** out, int device) {
         return HBG_E_DEVICE;
     }
     c->stream = c->own;
+    if (const char* e = getenv("HBG_TDEC_BATCHED")) c->tdec_batched = atoi(e) != 0;
     *out = c;
     return HBG_OK;
 }
@@ -512,6 +516,7 @@ namespace {
 struct CtTable {
     uint32_t *ct_u, *coefH, *coefW;
     int32_t* ct_status;
+    const uint8_t* U48;  // device copy of the compressed U points (batch weights hash them)
 };
 
 // Stage (host mode) and prepare a ciphertext table on the device.
@@ -543,9 +548,77 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     HBG_CHECK(scratch(c, 7, 4ull * bls::kLineWordsPerPoint * n_ct, &pwc));
     t.ct_u = (uint32_t*)pcu;
     t.ct_status = (int32_t*)pst;
+    t.U48 = dU;
     t.coefH = (uint32_t*)ph;
     t.coefW = (uint32_t*)pwc;
     HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW, c->stream));
+    return HBG_OK;
+}
+
+
+// Batched PublicKeyShare::verify_decryption_share (tdec_kernels.hip, "batched
+// share verification"): sort shares by ciphertext, cut batches of <= 64,
+// weighted batch sums, then three check rounds (batch, sub-batch of 8, single
+// share).  Host syncs: batch count, round-1 and round-2 list sizes.
+int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uint8_t* dU48, uint32_t n,
+                          const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp, const uint32_t* paff,
+                          const int32_t* pst, uint8_t* dok) {
+    void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
+    const size_t tb_bytes = bls::tdec_batch_temp_bytes(n);
+    HBG_CHECK(scratch(c, 16, 4ull * n, &keys));
+    HBG_CHECK(scratch(c, 17, 4ull * n, &perm));
+    HBG_CHECK(scratch(c, 18, 4ull * n, &ta));
+    HBG_CHECK(scratch(c, 19, 4ull * n, &tb));
+    HBG_CHECK(scratch(c, 20, (size_t)bls::kBatchDescBytes * n, &desc));
+    HBG_CHECK(scratch(c, 21, tb_bytes, &temp));
+    HBG_CHECK(scratch(c, 22, 64, &cnt));
+    uint32_t nbh[2] = {0, 0};
+    HBG_TRY(bls::launch_tdec_batch_plan(n, n_ct, dsc, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta, (uint32_t*)tb,
+                                        (bls::BatchDesc*)desc, temp, tb_bytes, nbh, c->stream));
+    const uint32_t nb = nbh[0] + nbh[1];
+    void *sums, *lok, *items, *fails;
+    HBG_CHECK(scratch(c, 23, (size_t)bls::kBatchSumBytes * nb, &sums));
+    HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
+    HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 8 * nb, &items));
+    HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
+    uint32_t* counts = (uint32_t*)cnt;  // [0] sub-batch items, [1] failing shares
+    HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
+    HBG_TRY(hipMemsetAsync(counts, 0, 8, c->stream));
+    HBG_TRY(bls::launch_tdec_batch_leaves(nb, (const bls::BatchDesc*)desc, (const uint32_t*)perm, dsh, dsp, dU48,
+                                          t.ct_status, paff, pst, (uint32_t*)sums, (uint8_t*)lok, c->stream));
+    // round 0: every batch sum
+    HBG_TRY(bls::launch_tdec_batch_check(nb, nullptr, (const bls::BatchDesc*)desc, (const uint32_t*)perm,
+                                         (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u, t.coefH, t.coefW, dok,
+                                         (bls::CheckItem*)items, counts, (uint32_t*)fails, counts + 1, c->stream));
+    uint32_t h[2];
+    HBG_TRY(hipMemcpyAsync(h, counts, 8, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    // round 1: sub-batches of failing batches (appends failing shares)
+    HBG_TRY(bls::launch_tdec_batch_check(h[0], (const bls::CheckItem*)items, (const bls::BatchDesc*)desc,
+                                         (const uint32_t*)perm, (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u,
+                                         t.coefH, t.coefW, dok, nullptr, nullptr, (uint32_t*)fails, counts + 1,
+                                         c->stream));
+    HBG_TRY(hipMemcpyAsync(h, counts, 8, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    if (getenv("HBG_TDEC_DEBUG")) {
+        fprintf(stderr, "hbg batched verify: n=%u batches=%u sub-items=%u fail-shares=%u\n", n, nb, h[0], h[1]);
+        std::vector<uint32_t> hd(4 * nb), hp(n);
+        std::vector<uint8_t> hl(64 * nb);
+        HBG_TRY(hipMemcpy(hd.data(), desc, 16ull * nb, hipMemcpyDeviceToHost));
+        HBG_TRY(hipMemcpy(hp.data(), perm, 4ull * n, hipMemcpyDeviceToHost));
+        HBG_TRY(hipMemcpy(hl.data(), lok, 64ull * nb, hipMemcpyDeviceToHost));
+        for (uint32_t b = 0; b < nb; ++b) {
+            fprintf(stderr, "  batch %u: start=%u end=%u ct=%u lok=", b, hd[4 * b], hd[4 * b + 1], hd[4 * b + 2]);
+            for (int l = 0; l < 64; ++l) fputc('0' + hl[64 * b + l], stderr);
+            fputc('\n', stderr);
+        }
+        fprintf(stderr, "  perm:");
+        for (uint32_t q = 0; q < n && q < 128; ++q) fprintf(stderr, " %u", hp[q]);
+        fputc('\n', stderr);
+    }
+    // round 2: the shares of failing sub-batches, one by one (the reference's equation)
+    HBG_TRY(bls::launch_tdec_verify_shares(h[1], dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff, pst, dok,
+                                           c->stream, (const uint32_t*)fails));
     return HBG_OK;
 }
 
@@ -592,8 +665,13 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
     HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
     HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
-    HBG_TRY(bls::launch_tdec_verify_shares(n, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, (uint32_t*)paff,
-                                           (int32_t*)pst, dok, c->stream));
+    if (c->tdec_batched && n >= 2 && n < (1ull << 31)) {
+        HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, dsh, dsc, dsp, (const uint32_t*)paff,
+                                        (const int32_t*)pst, dok));
+    } else {
+        HBG_TRY(bls::launch_tdec_verify_shares(n, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW,
+                                               (uint32_t*)paff, (int32_t*)pst, dok, c->stream));
+    }
     if (!(flags & HBG_DEVICE)) {
         HBG_TRY(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, c->stream));
         HBG_TRY(hipStreamSynchronize(c->stream));
@@ -670,6 +748,13 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
         return HBG_OK;
     }
     return finish(c, flags);
+}
+
+int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
+    if (!c) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->tdec_batched = on != 0;
+    return HBG_OK;
 }
 
 int hbg_test_bls(hbg_ctx* c, int op, uint32_t n, const uint32_t* in, uint32_t in_words, uint32_t* out,

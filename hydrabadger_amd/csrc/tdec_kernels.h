@@ -10,6 +10,11 @@ namespace bls {
 
 constexpr uint32_t kLineWordsPerPoint = 72 * 68;  // G2Prepared: 68 x (3 Fp2) x 12 u32
 constexpr uint32_t kAffWords = 32;                // affine record: x[12] y[12] flags
+constexpr uint32_t kBatchShares = 64;             // batched verification: shares per batch (8 x 8)
+
+struct BatchDesc;
+struct CheckItem;
+constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 9 * 2 * 36 * 4;
 
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
@@ -19,7 +24,21 @@ hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_
 hipError_t launch_tdec_verify_shares(uint64_t n, const uint8_t* share48, const uint32_t* share_ct,
                                      const uint32_t* share_pk, const uint32_t* ct_u, const int32_t* ct_status,
                                      const uint32_t* coefH, const uint32_t* coefW, const uint32_t* pk_aff,
-                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st);
+                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st,
+                                     const uint32_t* sel = nullptr);
+size_t tdec_batch_temp_bytes(uint32_t n);
+hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* share_ct, uint32_t* keys,
+                                  uint32_t* perm, uint32_t* tmp_a, uint32_t* tmp_b, BatchDesc* desc, void* temp,
+                                  size_t temp_bytes, uint32_t* nb_out, hipStream_t st);
+hipError_t launch_tdec_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share48,
+                                    const uint32_t* share_pk, const uint8_t* U48, const int32_t* ct_status,
+                                    const uint32_t* pk_aff, const int32_t* pk_status, uint32_t* sums,
+                                    uint8_t* leaf_ok, hipStream_t st);
+hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, const BatchDesc* desc,
+                                   const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
+                                   const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
+                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
+                                   hipStream_t st);
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,

@@ -20,6 +20,8 @@
 #include "keccak.h"
 #include "tdec_kernels.h"
 
+#include <hipcub/hipcub.hpp>
+
 namespace hbg {
 namespace bls {
 
@@ -312,9 +314,10 @@ __global__ __launch_bounds__(64) void tdec_verify_shares(uint64_t n, const uint8
                                                          const uint32_t* __restrict__ coefW,
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const int32_t* __restrict__ pk_status,
-                                                         uint8_t* __restrict__ ok) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
+                                                         uint8_t* __restrict__ ok, const uint32_t* __restrict__ sel) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = sel ? sel[i] : i;  // sel: share indices (batched path's failing leaves)
     const uint32_t ct = share_ct[k], pk = share_pk[k];
     bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
     G1A s;
@@ -328,6 +331,189 @@ __global__ __launch_bounds__(64) void tdec_verify_shares(uint64_t n, const uint8
                               coefW + (uint64_t)ct * 72 * kMillerSteps, pkx, pky, !pk_inf && !w_inf);
     }
     ok[k] = good ? 1 : 0;
+}
+
+
+// ---------------------------------------------------------------- batched share verification
+// verify_decryption_share for many shares of ONE ciphertext c shares (H, W):
+// e(S_i, H) == e(PK_i, W) for all i in a batch  <=  e(sum r_i S_i, H) ==
+// e(sum r_i PK_i, W) with 64-bit weights r_i derived from a digest of the
+// whole batch (Bellare-Garay-Rabin small-exponent batch test; a batch holding
+// an invalid share passes with probability <= 2^-63).  A batch is up to 64 shares of one
+// ciphertext, split in 8 sub-batches of 8: round 0 checks every batch sum, a
+// failing batch checks its sub-batch sums (round 1), a failing sub-batch
+// checks its shares one by one with the plain per-share test (round 2,
+// tdec_verify_shares) — so every reported 0 comes from the reference's own
+// per-share equation and every 1 from a passing (sub-)batch.
+struct BatchDesc {
+    uint32_t start, end, ct, pad;
+};
+struct CheckItem {
+    uint32_t b, node;  // node 0..7: sub-batch, 8: whole batch
+};
+constexpr uint32_t kJacWords = 36;                    // Jacobian G1: x, y, z
+constexpr uint32_t kSumWords = 2 * kJacWords;         // (sum r S, sum r PK)
+constexpr uint32_t kBatchSumWords = 9 * kSumWords;    // 8 sub-batch sums + batch sum
+
+__global__ void tdec_iota(uint32_t n, uint32_t* __restrict__ v) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
+// gs[q] = q where the (sorted) ciphertext key changes, else 0 (max-scan -> group start)
+__global__ void tdec_group_marks(uint32_t n, const uint32_t* __restrict__ key, uint32_t* __restrict__ gs) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) gs[q] = (q == 0 || key[q] != key[q - 1]) ? q : 0u;
+}
+
+__global__ void tdec_batch_heads(uint32_t n, const uint32_t* __restrict__ gs, uint32_t* __restrict__ head) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) head[q] = ((q - gs[q]) % kBatchShares == 0) ? 1u : 0u;
+}
+
+__global__ void tdec_batch_desc(uint32_t n, const uint32_t* __restrict__ key, const uint32_t* __restrict__ head,
+                                const uint32_t* __restrict__ bid, BatchDesc* __restrict__ desc) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const uint32_t b = bid[q] - 1u;  // bid: inclusive count of batch heads in [0, q]
+    if (head[q]) {
+        desc[b].start = q;
+        desc[b].ct = key[q];
+    }
+    if (q + 1 == n || head[q + 1]) desc[b].end = q + 1;
+}
+
+BD void store_jac(uint32_t* d, const G1& p) {
+    store_fp(d, p.x);
+    store_fp(d + 12, p.y);
+    store_fp(d + 24, p.z);
+}
+BD G1 load_jac(const uint32_t* d) { return {load_fp(d), load_fp(d + 12), load_fp(d + 24)}; }
+
+// One 64-lane block per batch: lane = share.  Decompress + subgroup check,
+// weight, and the 8 + 1 partial sums (LDS exchange).
+__global__ __launch_bounds__(64) void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
+                                                        const uint32_t* __restrict__ perm,
+                                                        const uint8_t* __restrict__ share48,
+                                                        const uint32_t* __restrict__ share_pk,
+                                                        const uint8_t* __restrict__ U48,
+                                                        const int32_t* __restrict__ ct_status,
+                                                        const uint32_t* __restrict__ pk_aff,
+                                                        const int32_t* __restrict__ pk_status,
+                                                        uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
+    __shared__ uint32_t sA[kBatchShares][kJacWords], sB[kBatchShares][kJacWords];
+    __shared__ uint32_t subA[8][kJacWords], subB[8][kJacWords];
+    __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    const BatchDesc d = desc[b];
+    const uint32_t q = d.start + lane;
+    const bool in = q < d.end;
+    const uint32_t k = in ? perm[q] : 0u;
+    const uint32_t pk = in ? share_pk[k] : 0u;
+    bool valid = in && ct_status[d.ct] == 0 && pk_status[pk] == 0;
+    G1A s;
+    if (valid) valid = g1_decompress(share48 + 48ull * k, s, true);
+    // Weights are bound to the WHOLE batch (Fiat-Shamir): leaf digest
+    // d_i = SHA3(U || S_i || pk_i), batch digest D = SHA3(d_0 || ... ),
+    // r_i = SHA3(D || i)[0..8] | 1 — changing any share re-randomises every
+    // weight, so shares cannot be ground against each other's weights.
+    if (in) {
+        uint8_t m[100];
+        for (int i = 0; i < 48; ++i) m[i] = U48[48ull * d.ct + i];
+        for (int i = 0; i < 48; ++i) m[48 + i] = share48[48ull * k + i];
+        for (int i = 0; i < 4; ++i) m[96 + i] = (uint8_t)(pk >> (8 * i));
+        sha3_bytes(m, 100, sDig + 32 * lane);
+    }
+    __syncthreads();
+    if (lane == 0) sha3_bytes(sDig, 32u * (d.end - d.start), sBatch);
+    __syncthreads();
+    G1 A = {fp_one(), fp_one(), fp_zero()}, B = A;
+    if (valid) {
+        uint8_t m[36], dg[32];
+        for (int i = 0; i < 32; ++i) m[i] = sBatch[i];
+        for (int i = 0; i < 4; ++i) m[32 + i] = (uint8_t)(lane >> (8 * i));
+        sha3_bytes(m, 36, dg);
+        uint64_t r = 0;
+        for (int i = 0; i < 8; ++i) r |= (uint64_t)dg[i] << (8 * i);
+        r |= 1ull;  // nonzero
+        if (!s.inf) A = g1_mul_u64(s.x, s.y, r);
+        const uint32_t* pa = pk_aff + 32ull * pk;
+        if (pa[24] == 0) B = g1_mul_u64(load_fp(pa), load_fp(pa + 12), r);
+    }
+    leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
+    for (int i = 0; i < 12; ++i) {
+        sA[lane][i] = A.x[i];
+        sA[lane][12 + i] = A.y[i];
+        sA[lane][24 + i] = A.z[i];
+        sB[lane][i] = B.x[i];
+        sB[lane][12 + i] = B.y[i];
+        sB[lane][24 + i] = B.z[i];
+    }
+    __syncthreads();
+    uint32_t* out = sums + (uint64_t)b * kBatchSumWords;
+    if (lane < 8) {
+        G1 a = load_jac(sA[8 * lane]), bb = load_jac(sB[8 * lane]);
+        for (int j = 1; j < 8; ++j) {
+            a = g1_add(a, load_jac(sA[8 * lane + j]));
+            bb = g1_add(bb, load_jac(sB[8 * lane + j]));
+        }
+        store_jac(out + lane * kSumWords, a);
+        store_jac(out + lane * kSumWords + kJacWords, bb);
+        store_jac(subA[lane], a);
+        store_jac(subB[lane], bb);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        G1 a = load_jac(subA[0]), bb = load_jac(subB[0]);
+        for (int j = 1; j < 8; ++j) {
+            a = g1_add(a, load_jac(subA[j]));
+            bb = g1_add(bb, load_jac(subB[j]));
+        }
+        store_jac(out + 8 * kSumWords, a);
+        store_jac(out + 8 * kSumWords + kJacWords, bb);
+    }
+}
+
+// One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.
+__global__ __launch_bounds__(64) void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict__ items,
+                                                       const BatchDesc* __restrict__ desc,
+                                                       const uint32_t* __restrict__ perm,
+                                                       const uint32_t* __restrict__ sums,
+                                                       const uint8_t* __restrict__ leaf_ok,
+                                                       const uint32_t* __restrict__ ct_u,
+                                                       const uint32_t* __restrict__ coefH,
+                                                       const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok,
+                                                       CheckItem* __restrict__ next, uint32_t* __restrict__ next_n,
+                                                       uint32_t* __restrict__ fail_list,
+                                                       uint32_t* __restrict__ fail_n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_items) return;
+    const CheckItem it = items ? items[i] : CheckItem{i, 8u};
+    const BatchDesc d = desc[it.b];
+    const uint32_t l0 = it.node == 8 ? 0u : 8u * it.node, l1 = it.node == 8 ? kBatchShares : l0 + 8u;
+    const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
+    bool any = false;
+    for (uint32_t l = l0; l < l1; ++l) any |= lok[l] != 0;
+    if (!any) return;  // nothing valid to vouch for: those shares stay 0
+    const uint32_t* sm = sums + (uint64_t)it.b * kBatchSumWords + it.node * kSumWords;
+    const G1A a = g1_to_affine(load_jac(sm)), bb = g1_to_affine(load_jac(sm + kJacWords));
+    const bool w_inf = ct_u[32ull * d.ct + 25] != 0;
+    const bool pass = pairing_check2(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, !a.inf,
+                                     coefW + (uint64_t)d.ct * kLineWordsPerPoint, bb.x, fp_neg(bb.y),
+                                     !bb.inf && !w_inf);
+    if (pass) {
+        for (uint32_t l = l0; l < l1; ++l)
+            if (lok[l]) ok[perm[d.start + l]] = 1;
+    } else if (it.node == 8) {
+        for (uint32_t sb = 0; sb < 8; ++sb) {
+            bool v = false;
+            for (uint32_t l = 8 * sb; l < 8 * sb + 8; ++l) v |= lok[l] != 0;
+            if (v) next[atomicAdd(next_n, 1u)] = CheckItem{it.b, sb};
+        }
+    } else {
+        for (uint32_t l = l0; l < l1; ++l)
+            if (lok[l]) fail_list[atomicAdd(fail_n, 1u)] = perm[d.start + l];
+    }
 }
 
 __global__ __launch_bounds__(64) void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
@@ -503,6 +689,7 @@ __global__ __launch_bounds__(64) void tdec_combine(uint32_t n, uint32_t t, const
 // ------------------------------------------------------------------ unit-test hook
 // op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
+//     9 [k]P (64-bit k)  10 P + Q (Jacobian add)
 // Field values cross the boundary as canonical raw limbs (12 u32 LE).
 __global__ __launch_bounds__(64) void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
                                                 uint32_t* __restrict__ out, uint32_t in_words,
@@ -558,6 +745,20 @@ __global__ __launch_bounds__(64) void tdec_test(int op, uint32_t n, const uint32
         st(12, h.x.c1);
         st(24, h.y.c0);
         st(36, h.y.c1);
+    } else if (op == 9) {
+        // in: P.x P.y k_lo k_hi -> affine [k]P (x, y, inf)
+        const uint64_t kk = (uint64_t)a[24] | ((uint64_t)a[25] << 32);
+        const G1A r = g1_to_affine(g1_mul_u64(ld(0), ld(12), kk));
+        st(0, r.x);
+        st(12, r.y);
+        o[24] = r.inf;
+    } else if (op == 10) {
+        // in: P.x P.y Q.x Q.y (affine, Z = 1) -> affine P + Q via the Jacobian g1_add
+        const G1 p = {ld(0), ld(12), fp_one()}, q = {ld(24), ld(36), fp_one()};
+        const G1A r = g1_to_affine(g1_add(p, q));
+        st(0, r.x);
+        st(12, r.y);
+        o[24] = r.inf;
     } else if (op == 8) {
         Fp12 f;
         Fp* c[12] = {&f.c0.c0.c0, &f.c0.c0.c1, &f.c0.c1.c0, &f.c0.c1.c1, &f.c0.c2.c0, &f.c0.c2.c1,
@@ -583,9 +784,68 @@ hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_
 hipError_t launch_tdec_verify_shares(uint64_t n, const uint8_t* share48, const uint32_t* share_ct,
                                      const uint32_t* share_pk, const uint32_t* ct_u, const int32_t* ct_status,
                                      const uint32_t* coefH, const uint32_t* coefW, const uint32_t* pk_aff,
-                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st) {
+                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st, const uint32_t* sel) {
+    if (n == 0) return hipSuccess;
     tdec_verify_shares<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(
-        n, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok);
+        n, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok, sel);
+    return hipGetLastError();
+}
+
+// ---- batched verification host driver pieces
+size_t tdec_batch_temp_bytes(uint32_t n) {
+    size_t a = 0, b = 0, c = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+    (void)hipcub::DeviceScan::InclusiveScan(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr, hipcub::Max(),
+                                            (int)n);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+    return (a > b ? (a > c ? a : c) : (b > c ? b : c)) + 256;
+}
+
+// Sort shares by ciphertext (stable), cut batches; bid_n <- number of batches (device word).
+hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* share_ct, uint32_t* keys,
+                                  uint32_t* perm, uint32_t* tmp_a, uint32_t* tmp_b, BatchDesc* desc, void* temp,
+                                  size_t temp_bytes, uint32_t* nb_out, hipStream_t st) {
+    const dim3 g((n + 255) / 256), blk(256);
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < n_ct) ++bits;
+    tdec_iota<<<g, blk, 0, st>>>(n, tmp_a);
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, share_ct, keys, tmp_a, perm, (int)n, 0, bits,
+                                                      st);
+    if (e != hipSuccess) return e;
+    tdec_group_marks<<<g, blk, 0, st>>>(n, keys, tmp_a);
+    e = hipcub::DeviceScan::InclusiveScan(temp, temp_bytes, tmp_a, tmp_b, hipcub::Max(), (int)n, st);
+    if (e != hipSuccess) return e;
+    tdec_batch_heads<<<g, blk, 0, st>>>(n, tmp_b, tmp_a);            // tmp_a = head flags
+    e = hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, tmp_a, tmp_b, (int)n, st);  // tmp_b = batch id + 1
+    if (e != hipSuccess) return e;
+    tdec_batch_desc<<<g, blk, 0, st>>>(n, keys, tmp_a, tmp_b, desc);
+    // number of batches = heads in [0, n)
+    e = hipMemcpyAsync(nb_out, tmp_b + (n - 1), 4, hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return e;
+    nb_out[1] = 0;
+    return hipStreamSynchronize(st);
+}
+
+hipError_t launch_tdec_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share48,
+                                    const uint32_t* share_pk, const uint8_t* U48, const int32_t* ct_status,
+                                    const uint32_t* pk_aff, const int32_t* pk_status, uint32_t* sums,
+                                    uint8_t* leaf_ok, hipStream_t st) {
+    if (nb == 0) return hipSuccess;
+    tdec_batch_leaves<<<dim3(nb), dim3(64), 0, st>>>(desc, perm, share48, share_pk, U48, ct_status, pk_aff, pk_status,
+                                                     sums, leaf_ok);
+    return hipGetLastError();
+}
+
+hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, const BatchDesc* desc,
+                                   const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
+                                   const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
+                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
+                                   hipStream_t st) {
+    if (n_items == 0) return hipSuccess;
+    tdec_batch_check<<<dim3((n_items + 63) / 64), dim3(64), 0, st>>>(n_items, items, desc, perm, sums, leaf_ok, ct_u,
+                                                                     coefH, coefW, ok, next, next_n, fail_list,
+                                                                     fail_n);
     return hipGetLastError();
 }
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,

@@ -11,6 +11,10 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* Choose the share-verification schedule of hbg_tdec_verify_shares: 1 (the
+ * default) batched small-exponent test with per-share fallback, 0 one
+ * independent pairing check per share.  Both return identical bits. */
+int hbg_test_set_tdec_batched(hbg_ctx *ctx, int on);
 int hbg_test_bls(hbg_ctx *ctx, int op, uint32_t n, const uint32_t *in, uint32_t in_words, uint32_t *out,
                  uint32_t out_words);
 #ifdef __cplusplus

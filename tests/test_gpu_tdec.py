@@ -238,3 +238,78 @@ def test_golden_tdec_on_gpu():
                                         for c in sc["cts"]])
     assert st.tolist() == [0] * len(cts)
     assert [p.hex() for p in pts] == [c["plaintext"] for c in sc["cts"]]
+
+
+@pytest.mark.parametrize("bad_rate,seed", [(0.0, 1), (0.03, 2), (0.3, 3)])
+def test_batched_verify_equals_per_share(bad_rate, seed):
+    """hbg_tdec_verify_shares' batched schedule (weighted batch sums per
+    ciphertext, sub-batches of 8, per-share fallback) returns exactly the bits
+    of one pairing check per share — on the N=64 t=21 fixture's 4 ciphertexts
+    x 64 shares, replicated to 150 ciphertexts (ragged last batches: 150*64
+    shares in shuffled order, so batches cut mid-group), with a seeded fraction
+    of shares claimed under the wrong key or corrupted, plus invalid
+    encodings and out-of-subgroup / identity shares."""
+    import json
+    import os
+    from hydrabadger_amd import _lib
+    th = _th()
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tdec_n64.json")))["scenario"]
+    K, n = len(g["cts"]), len(g["pk_shares"])
+    n_ct = 150
+    cts = [th.Ciphertext(bytes.fromhex(g["cts"][j % K]["U"]), bytes.fromhex(g["cts"][j % K]["V"]),
+                         bytes.fromhex(g["cts"][j % K]["W"])) for j in range(n_ct)]
+    pk = [bytes.fromhex(p) for p in g["pk_shares"]]
+    rng = np.random.default_rng(seed)
+    items, expect = [], []
+    for j in range(n_ct):
+        for i in range(n if j < n_ct - 1 else 37):          # ragged last ciphertext
+            sh = bytes.fromhex(g["cts"][j % K]["shares"][i])
+            r = rng.random()
+            if r < bad_rate / 2:
+                items.append((sh, j, (i + 1) % n)); expect.append(0)        # wrong key
+            elif r < bad_rate:
+                other = bytes.fromhex(g["cts"][(j + 1) % K]["shares"][i])
+                items.append((other, j, i)); expect.append(0)              # share of another ct
+            else:
+                items.append((sh, j, i)); expect.append(1)
+    junk = bytearray(items[5][0]); junk[0] &= 0x7F                            # invalid encoding
+    items.append((bytes(junk), 3, 5)); expect.append(0)
+    items.append((B.g1_compress(B.G1), 7, 9)); expect.append(0)               # valid point, wrong share
+    order = rng.permutation(len(items))
+    items = [items[k] for k in order]
+    expect = np.array([expect[k] for k in order], np.uint8)
+    ctx = _lib.Context(0)
+    try:
+        outs = []
+        for mode in (1, 0):
+            _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
+            outs.append(th.verify_shares_batch(cts, pk, items, ctx))
+    finally:
+        ctx.close()
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], expect)
+
+
+def test_g1_mul_u64_and_add():
+    """Device G1 scalar multiplication by 64-bit weights and Jacobian addition
+    (the batched verifier's building blocks) against the oracle."""
+    th = _th()
+    pts = [B.G1, B.g1_mul(B.G1, 7), B.g1_mul(B.G1, 2 ** 200 + 12345)]
+    ks = [1, 2, 3, 0xFFFFFFFFFFFFFFFF, 0x8000000000000001, 0x123456789ABCDEF1]
+    rows, ref = [], []
+    for p in pts:
+        for k in ks:
+            rows.append(limbs(p[0]) + limbs(p[1]) + [k & 0xFFFFFFFF, k >> 32])
+            ref.append(B.g1_mul(p, k))
+    out = th.test_bls(9, np.array(rows, np.uint32), 25)
+    for o, r in zip(out, ref):
+        assert (from_limbs(o[:12]), from_limbs(o[12:24])) == r and o[24] == 0
+    pairs = [(pts[0], pts[1]), (pts[1], pts[1]), (pts[2], B.g1_neg(pts[2])), (pts[1], pts[2])]
+    out = th.test_bls(10, np.array([limbs(p[0]) + limbs(p[1]) + limbs(q[0]) + limbs(q[1]) for p, q in pairs],
+                                   np.uint32), 25)
+    for o, (p, q) in zip(out, pairs):
+        r = B.g1_add(p, q)
+        if r is None:
+            assert o[24] == 1
+        else:
+            assert (from_limbs(o[:12]), from_limbs(o[12:24])) == r and o[24] == 0
