@@ -41,7 +41,9 @@ struct hbg_ctx {
     Buf slot[kNumSlots];
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> matrices;  // device (D+Q) x D coding matrices
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> enc_plans; // device shared encode plans
-    int tdec_batched = 1;  // batched share verification (hbg_test_set_tdec_batched / HBG_TDEC_BATCHED=0)
+    // share verification schedule (hbg_test_set_tdec_batched / HBG_TDEC_BATCHED): 0 per share, 1 batched
+    // (pk fixed-base tables when each key verifies >= kPkTableMinUses shares), 2 batched + tables always
+    int tdec_batched = 1;
     std::mutex mu;
 };
 
@@ -245,7 +247,7 @@ int hbg_init(hbg_ctx** out, int device) {
         return HBG_E_DEVICE;
     }
     c->stream = c->own;
-    if (const char* e = getenv("HBG_TDEC_BATCHED")) c->tdec_batched = atoi(e) != 0;
+    if (const char* e = getenv("HBG_TDEC_BATCHED")) c->tdec_batched = atoi(e);
     *out = c;
     return HBG_OK;
 }
@@ -560,9 +562,20 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
 // share verification"): sort shares by ciphertext, cut batches of <= 64,
 // weighted batch sums, then three check rounds (batch, sub-batch of 8, single
 // share).  Host syncs: batch count, round-1 and round-2 list sizes.
+// A pk table costs ~2k G1 scalar multiplications to build and saves ~60 G1
+// doublings per share verified under that key.
+constexpr uint64_t kPkTableMinUses = 2048;
+
 int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uint8_t* dU48, uint32_t n,
-                          const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp, const uint32_t* paff,
-                          const int32_t* pst, uint8_t* dok) {
+                          uint32_t n_pk, const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp,
+                          const uint32_t* paff, const int32_t* pst, uint8_t* dok) {
+    uint32_t* tbl = nullptr;
+    if (c->tdec_batched == 2 || (uint64_t)n >= kPkTableMinUses * n_pk) {
+        void* p;
+        HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
+        tbl = (uint32_t*)p;
+        HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream));
+    }
     void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
     const size_t tb_bytes = bls::tdec_batch_temp_bytes(n);
     HBG_CHECK(scratch(c, 16, 4ull * n, &keys));
@@ -585,7 +598,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
     HBG_TRY(hipMemsetAsync(counts, 0, 8, c->stream));
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, (const bls::BatchDesc*)desc, (const uint32_t*)perm, dsh, dsp, dU48,
-                                          t.ct_status, paff, pst, (uint32_t*)sums, (uint8_t*)lok, c->stream));
+                                          t.ct_status, paff, pst, tbl, (uint32_t*)sums, (uint8_t*)lok, c->stream));
     // round 0: every batch sum
     HBG_TRY(bls::launch_tdec_batch_check(nb, nullptr, (const bls::BatchDesc*)desc, (const uint32_t*)perm,
                                          (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u, t.coefH, t.coefW, dok,
@@ -666,7 +679,7 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
     HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
     if (c->tdec_batched && n >= 2 && n < (1ull << 31)) {
-        HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, dsh, dsc, dsp, (const uint32_t*)paff,
+        HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, n_pk, dsh, dsc, dsp, (const uint32_t*)paff,
                                         (const int32_t*)pst, dok));
     } else {
         HBG_TRY(bls::launch_tdec_verify_shares(n, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW,
@@ -753,7 +766,8 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    c->tdec_batched = on != 0;
+    if (on < 0 || on > 2) return HBG_E_ARG;
+    c->tdec_batched = on;
     return HBG_OK;
 }
 

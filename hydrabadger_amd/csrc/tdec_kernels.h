@@ -32,8 +32,10 @@ hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* sha
                                   size_t temp_bytes, uint32_t* nb_out, hipStream_t st);
 hipError_t launch_tdec_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share48,
                                     const uint32_t* share_pk, const uint8_t* U48, const int32_t* ct_status,
-                                    const uint32_t* pk_aff, const int32_t* pk_status, uint32_t* sums,
-                                    uint8_t* leaf_ok, hipStream_t st);
+                                    const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* pk_tbl,
+                                    uint32_t* sums, uint8_t* leaf_ok, hipStream_t st);
+size_t tdec_pk_table_bytes(uint32_t n_pk);
+hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st);
 hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, const BatchDesc* desc,
                                    const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
                                    const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,

@@ -390,8 +390,38 @@ BD void store_jac(uint32_t* d, const G1& p) {
 }
 BD G1 load_jac(const uint32_t* d) { return {load_fp(d), load_fp(d + 12), load_fp(d + 24)}; }
 
+BD G1 g1_shfl_xor(const G1& p, int m) {
+    G1 r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        r.x[i] = __shfl_xor(p.x[i], m);
+        r.y[i] = __shfl_xor(p.y[i], m);
+        r.z[i] = __shfl_xor(p.z[i], m);
+    }
+    return r;
+}
+
+// Fixed-base tables of the public key shares for the batch weights:
+// tbl[pk][w][v] = affine [v * 2^(8w)] PK_pk, v in 1..255, w in 0..7 (v = 0
+// unused), so [r] PK for a 64-bit weight is 8 mixed additions, no doublings.
+constexpr uint32_t kPkTblWords = 8 * 256 * 24;
+__global__ __launch_bounds__(64) void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
+                                                    uint32_t* __restrict__ tbl) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // (pk, w, v)
+    if (i >= n_pk * 2048u) return;
+    const uint32_t pk = i >> 11, w = (i >> 8) & 7u, v = i & 255u;
+    const uint32_t* pa = pk_aff + 32ull * pk;
+    uint32_t* o = tbl + (uint64_t)pk * kPkTblWords + (uint64_t)(w * 256 + v) * 24;
+    if (v == 0 || pa[24] != 0) return;
+    const G1A r = g1_to_affine(g1_mul_u64(load_fp(pa), load_fp(pa + 12), (uint64_t)v << (8 * w)));
+    store_fp(o, r.x);
+    store_fp(o + 12, r.y);
+}
+
 // One 64-lane block per batch: lane = share.  Decompress + subgroup check,
-// weight, and the 8 + 1 partial sums (LDS exchange).
+// weight, and the 8 sub-batch sums + the batch sum by cross-lane butterfly
+// (ds_swizzle/bpermute shuffles: no LDS for the points, so occupancy is set
+// by VGPRs alone).
 __global__ __launch_bounds__(64) void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
                                                         const uint32_t* __restrict__ perm,
                                                         const uint8_t* __restrict__ share48,
@@ -400,9 +430,8 @@ __global__ __launch_bounds__(64) void tdec_batch_leaves(const BatchDesc* __restr
                                                         const int32_t* __restrict__ ct_status,
                                                         const uint32_t* __restrict__ pk_aff,
                                                         const int32_t* __restrict__ pk_status,
+                                                        const uint32_t* __restrict__ pk_tbl,
                                                         uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
-    __shared__ uint32_t sA[kBatchShares][kJacWords], sB[kBatchShares][kJacWords];
-    __shared__ uint32_t subA[8][kJacWords], subB[8][kJacWords];
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     const BatchDesc d = desc[b];
@@ -438,39 +467,35 @@ __global__ __launch_bounds__(64) void tdec_batch_leaves(const BatchDesc* __restr
         r |= 1ull;  // nonzero
         if (!s.inf) A = g1_mul_u64(s.x, s.y, r);
         const uint32_t* pa = pk_aff + 32ull * pk;
-        if (pa[24] == 0) B = g1_mul_u64(load_fp(pa), load_fp(pa + 12), r);
+        if (pa[24] == 0) {
+            if (pk_tbl) {
+                const uint32_t* t = pk_tbl + (uint64_t)pk * kPkTblWords;
+                for (int w = 0; w < 8; ++w) {
+                    const uint32_t v = (uint32_t)(r >> (8 * w)) & 255u;
+                    if (v) {
+                        const uint32_t* e = t + (w * 256 + v) * 24;
+                        B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+                    }
+                }
+            } else {
+                B = g1_mul_u64(load_fp(pa), load_fp(pa + 12), r);
+            }
+        }
     }
     leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
-    for (int i = 0; i < 12; ++i) {
-        sA[lane][i] = A.x[i];
-        sA[lane][12 + i] = A.y[i];
-        sA[lane][24 + i] = A.z[i];
-        sB[lane][i] = B.x[i];
-        sB[lane][12 + i] = B.y[i];
-        sB[lane][24 + i] = B.z[i];
-    }
-    __syncthreads();
     uint32_t* out = sums + (uint64_t)b * kBatchSumWords;
-    if (lane < 8) {
-        G1 a = load_jac(sA[8 * lane]), bb = load_jac(sB[8 * lane]);
-        for (int j = 1; j < 8; ++j) {
-            a = g1_add(a, load_jac(sA[8 * lane + j]));
-            bb = g1_add(bb, load_jac(sB[8 * lane + j]));
+#pragma unroll 1
+    for (int m = 1; m < 64; m <<= 1) {
+        A = g1_add(A, g1_shfl_xor(A, m));
+        B = g1_add(B, g1_shfl_xor(B, m));
+        if (m == 4 && (lane & 7u) == 0) {  // sub-batch sums
+            store_jac(out + (lane >> 3) * kSumWords, A);
+            store_jac(out + (lane >> 3) * kSumWords + kJacWords, B);
         }
-        store_jac(out + lane * kSumWords, a);
-        store_jac(out + lane * kSumWords + kJacWords, bb);
-        store_jac(subA[lane], a);
-        store_jac(subB[lane], bb);
     }
-    __syncthreads();
     if (lane == 0) {
-        G1 a = load_jac(subA[0]), bb = load_jac(subB[0]);
-        for (int j = 1; j < 8; ++j) {
-            a = g1_add(a, load_jac(subA[j]));
-            bb = g1_add(bb, load_jac(subB[j]));
-        }
-        store_jac(out + 8 * kSumWords, a);
-        store_jac(out + 8 * kSumWords + kJacWords, bb);
+        store_jac(out + 8 * kSumWords, A);
+        store_jac(out + 8 * kSumWords + kJacWords, B);
     }
 }
 
@@ -686,6 +711,78 @@ __global__ __launch_bounds__(64) void tdec_combine(uint32_t n, uint32_t t, const
     for (uint64_t i = 0; i < len; ++i) out[off + i] = V[off + i] ^ (uint8_t)(rng.next_u32() & 0xFFu);
 }
 
+// [l]P for a 255-bit canonical scalar (8 LE words), P affine: double-and-add.
+BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
+    G1 r = {fp_one(), fp_one(), fp_zero()};
+    int top = 254;
+    while (top >= 0 && !((l[top >> 5] >> (top & 31)) & 1u)) --top;
+    for (int bit = top; bit >= 0; --bit) {
+        r = g1_dbl(r);
+        if ((l[bit >> 5] >> (bit & 31)) & 1u) r = g1_add_mixed(r, px, py);
+    }
+    return r;
+}
+
+// PublicKeySet::decrypt with one 32-lane group per ciphertext (t + 1 <= 32):
+// lane i owns share i — DuplicateEntry / decode checks, its Lagrange
+// coefficient lambda_i (one Fr inversion per lane) and [lambda_i] S_i — then a
+// 5-level butterfly sums the group and lane 0 hashes and XORs.  Same sum, same
+// error precedence (DuplicateEntry before an undecodable share) as the
+// one-lane-per-ciphertext tdec_combine; 22x the parallelism at N=64 t=21.
+__global__ __launch_bounds__(64) void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
+                                                       const uint32_t* __restrict__ idx,
+                                                       const uint8_t* __restrict__ V,
+                                                       const uint64_t* __restrict__ V_off,
+                                                       uint8_t* __restrict__ out, int32_t* __restrict__ status) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+    const uint32_t i = threadIdx.x & 31u, half = threadIdx.x & 32u;
+    const uint32_t m = t + 1;
+    const bool live = g < n;  // no early return: the group shuffles below need every lane
+    const bool act = live && i < m;
+    const uint32_t* ix = idx + (uint64_t)(live ? g : 0) * m;
+    const uint32_t me = act ? ix[i] : 0u;
+    bool dup = false;
+    if (act)
+        for (uint32_t j = i + 1; j < m; ++j) dup |= ix[j] == me;
+    G1A p = {fp_zero(), fp_zero(), true};
+    bool bad = false;
+    if (act) bad = !g1_decompress(share48 + ((uint64_t)g * m + i) * 48, p, false);
+    const uint32_t any_dup = (uint32_t)(__ballot(dup) >> half);
+    const uint32_t any_bad = (uint32_t)(__ballot(bad) >> half);
+    const int32_t st = any_dup ? HBG_E_DUPLICATE_ENTRY : (any_bad ? HBG_E_INVALID_POINT : 0);
+    G1 acc = {fp_one(), fp_one(), fp_zero()};
+    if (act && st == 0 && !p.inf) {
+        // lambda_i = prod_{j != i} x_j / prod_{j != i} (x_j - x_i),  x = index + 1  (mod r)
+        Fr num = fr_from_u32(1), den = fr_from_u32(1);
+        const Fr xi = fr_from_u32(me + 1);
+        for (uint32_t j = 0; j < m; ++j) {
+            if (j == i) continue;
+            const Fr xj = fr_from_u32(ix[j] + 1);
+            num = fr_mul(num, xj);
+            den = fr_mul(den, fr_sub(xj, xi));
+        }
+        const Fr l = fr_canonical(fr_mul(num, fr_inv(den)));
+        uint32_t lw[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) lw[w] = l.v[w];
+        acc = g1_mul_fr(p.x, p.y, lw);
+    }
+#pragma unroll 1
+    for (int s = 1; s < 32; s <<= 1) acc = g1_add(acc, g1_shfl_xor(acc, s));
+    if (!live || i != 0) return;
+    status[g] = st;
+    if (st != 0) return;
+    const G1A sum = g1_to_affine(acc);
+    uint8_t cg[48];
+    g1_compress(cg, sum);
+    uint8_t seed[32];
+    sha3_bytes(cg, 48, seed);
+    ChaChaRng rng;
+    rng.init(seed);
+    const uint64_t off = V_off[g], len = V_off[g + 1] - off;
+    for (uint64_t b = 0; b < len; ++b) out[off + b] = V[off + b] ^ (uint8_t)(rng.next_u32() & 0xFFu);
+}
+
 // ------------------------------------------------------------------ unit-test hook
 // op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
@@ -829,11 +926,19 @@ hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* sha
 
 hipError_t launch_tdec_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share48,
                                     const uint32_t* share_pk, const uint8_t* U48, const int32_t* ct_status,
-                                    const uint32_t* pk_aff, const int32_t* pk_status, uint32_t* sums,
-                                    uint8_t* leaf_ok, hipStream_t st) {
+                                    const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* pk_tbl,
+                                    uint32_t* sums, uint8_t* leaf_ok, hipStream_t st) {
     if (nb == 0) return hipSuccess;
     tdec_batch_leaves<<<dim3(nb), dim3(64), 0, st>>>(desc, perm, share48, share_pk, U48, ct_status, pk_aff, pk_status,
-                                                     sums, leaf_ok);
+                                                     pk_tbl, sums, leaf_ok);
+    return hipGetLastError();
+}
+
+size_t tdec_pk_table_bytes(uint32_t n_pk) { return 4ull * kPkTblWords * n_pk; }
+
+hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st) {
+    if (n_pk == 0) return hipSuccess;
+    tdec_pk_table<<<dim3((n_pk * 2048u + 63) / 64), dim3(64), 0, st>>>(n_pk, pk_aff, tbl);
     return hipGetLastError();
 }
 
@@ -856,7 +961,11 @@ hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, hipStream_t st) {
-    tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status, scratch);
+    if (n == 0) return hipSuccess;
+    if (t + 1 <= 32)
+        tdec_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status);
+    else
+        tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status, scratch);
     return hipGetLastError();
 }
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,

@@ -12,8 +12,10 @@
 extern "C" {
 #endif
 /* Choose the share-verification schedule of hbg_tdec_verify_shares: 1 (the
- * default) batched small-exponent test with per-share fallback, 0 one
- * independent pairing check per share.  Both return identical bits. */
+ * default) batched small-exponent test with per-share fallback (public-key
+ * fixed-base tables when each key verifies >= 2048 shares), 2 the same with
+ * the tables always built, 0 one independent pairing check per share.  All
+ * return identical bits. */
 int hbg_test_set_tdec_batched(hbg_ctx *ctx, int on);
 int hbg_test_bls(hbg_ctx *ctx, int op, uint32_t n, const uint32_t *in, uint32_t in_words, uint32_t *out,
                  uint32_t out_words);

@@ -281,12 +281,13 @@ def test_batched_verify_equals_per_share(bad_rate, seed):
     ctx = _lib.Context(0)
     try:
         outs = []
-        for mode in (1, 0):
+        for mode in (1, 2, 0):
             _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
             outs.append(th.verify_shares_batch(cts, pk, items, ctx))
     finally:
         ctx.close()
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[2])
+    assert np.array_equal(outs[1], outs[2])
     assert np.array_equal(outs[0], expect)
 
 
@@ -313,3 +314,44 @@ def test_g1_mul_u64_and_add():
             assert o[24] == 1
         else:
             assert (from_limbs(o[:12]), from_limbs(o[12:24])) == r and o[24] == 0
+
+
+@pytest.mark.parametrize("t", [0, 5, 21, 31, 40])
+def test_combine_kernels_interpolate_arbitrary_points(t):
+    """hbg_tdec_combine over arbitrary G1 points (interpolation does not care
+    whether shares are valid): t + 1 <= 32 runs the 32-lane-group kernel, t = 40
+    the one-lane-per-ciphertext kernel.  Shuffled sparse indices, identity
+    shares, an odd ciphertext count (half-live last group), and per-ciphertext
+    DuplicateEntry / undecodable-share statuses in the same call."""
+    from hydrabadger_amd import _lib
+    th = _th()
+    rng = random.Random(1000 + t)
+    n_ct = 5
+    cts_o, items, expect = [], [], []
+    for c in range(n_ct):
+        U = B.g1_mul(B.G1, rng.randrange(1, B.R))
+        V = bytes(rng.randrange(256) for _ in range(rng.choice([0, 7, 64, 65, 300])))
+        W = B.g2_mul(B.G2, rng.randrange(1, B.R))
+        cts_o.append(T.Ciphertext(U, V, W))
+        ids = rng.sample(range(200), t + 1)
+        pts = [None if (j == 1 and c == 2) else B.g1_mul(B.G1, rng.randrange(1, B.R)) for j in range(t + 1)]
+        it = [(i, B.g1_compress(p)) for i, p in zip(ids, pts)]
+        st = 0
+        if c == 3 and t > 0:
+            it[-1] = (it[0][0], it[-1][1])            # duplicate index -> DuplicateEntry
+            st = 1
+        if c == 4:
+            junk = bytearray(it[0][1]); junk[0] &= 0x7F  # undecodable share
+            it[0] = (it[0][0], bytes(junk))
+            st = 2 if st == 0 else st
+        items.append(it)
+        expect.append((st, None if st else T.decrypt(t, list(zip(ids, pts)), cts_o[-1])))
+    cts = [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in cts_o]
+    pts_out, status = th.combine_batch(t, cts, items)
+    for c, (st, pt) in enumerate(expect):
+        if st == 0:
+            assert status[c] == 0 and pts_out[c] == pt, c
+        elif st == 1:
+            assert status[c] == _lib.HBG_E_DUPLICATE_ENTRY, c
+        else:
+            assert status[c] == _lib.HBG_E_INVALID_POINT, c
