@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libhbgpu.so")
+LIB_PATH = os.environ.get("HBG_LIB_PATH") or os.path.join(_PKG, "libhbgpu.so")  # override: A/B experiments only
 
 HBG_OK = 0
 HBG_E_ARG = -1

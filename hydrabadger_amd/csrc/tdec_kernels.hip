@@ -25,6 +25,16 @@
 namespace hbg {
 namespace bls {
 
+// Occupancy contract for every TDec kernel: the tower arithmetic is a deep
+// non-inlined call graph whose callees otherwise take the whole 512-entry
+// unified register file (256 VGPRs + AGPR spill space = 1 wave/SIMD).  Capping
+// every kernel (and so, via attribute propagation, every callee) at
+// HBG_TDEC_WPE waves per SIMD trades a few scratch spills for latency hiding.
+#ifndef HBG_TDEC_WPE
+#define HBG_TDEC_WPE 2
+#endif
+#define TDEC_KERNEL __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HBG_TDEC_WPE)))
+
 #define BD __device__ __forceinline__
 
 // ------------------------------------------------------------------ SHA3-256 over bytes
@@ -253,7 +263,7 @@ BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool us
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(64) void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
+TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
                                                       const uint8_t* __restrict__ V,
                                                       const uint64_t* __restrict__ V_off,
                                                       const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(64) void tdec_ct_prepare(uint32_t n, const uint8_t*
     if (!w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
 }
 
-__global__ __launch_bounds__(64) void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
+TDEC_KERNEL void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
                                                       uint32_t* __restrict__ pk_aff, int32_t* __restrict__ pk_status) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(64) void tdec_pk_prepare(uint32_t n, const uint8_t*
     pk_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
 }
 
-__global__ __launch_bounds__(64) void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ share48,
+TDEC_KERNEL void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ share48,
                                                          const uint32_t* __restrict__ share_ct,
                                                          const uint32_t* __restrict__ share_pk,
                                                          const uint32_t* __restrict__ ct_u,
@@ -405,7 +415,7 @@ BD G1 g1_shfl_xor(const G1& p, int m) {
 // tbl[pk][w][v] = affine [v * 2^(8w)] PK_pk, v in 1..255, w in 0..7 (v = 0
 // unused), so [r] PK for a 64-bit weight is 8 mixed additions, no doublings.
 constexpr uint32_t kPkTblWords = 8 * 256 * 24;
-__global__ __launch_bounds__(64) void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
+TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
                                                     uint32_t* __restrict__ tbl) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // (pk, w, v)
     if (i >= n_pk * 2048u) return;
@@ -422,7 +432,7 @@ __global__ __launch_bounds__(64) void tdec_pk_table(uint32_t n_pk, const uint32_
 // weight, and the 8 sub-batch sums + the batch sum by cross-lane butterfly
 // (ds_swizzle/bpermute shuffles: no LDS for the points, so occupancy is set
 // by VGPRs alone).
-__global__ __launch_bounds__(64) void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
+TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
                                                         const uint32_t* __restrict__ perm,
                                                         const uint8_t* __restrict__ share48,
                                                         const uint32_t* __restrict__ share_pk,
@@ -500,7 +510,7 @@ __global__ __launch_bounds__(64) void tdec_batch_leaves(const BatchDesc* __restr
 }
 
 // One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.
-__global__ __launch_bounds__(64) void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict__ items,
+TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict__ items,
                                                        const BatchDesc* __restrict__ desc,
                                                        const uint32_t* __restrict__ perm,
                                                        const uint32_t* __restrict__ sums,
@@ -541,7 +551,7 @@ __global__ __launch_bounds__(64) void tdec_batch_check(uint32_t n_items, const C
     }
 }
 
-__global__ __launch_bounds__(64) void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
+TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
                                                      const int32_t* __restrict__ ct_status,
                                                      const uint32_t* __restrict__ coefH,
                                                      const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok) {
@@ -645,7 +655,7 @@ BD Fr fr_canonical(const Fr& a) {
 // PublicKeySet::decrypt for one ciphertext per work-item.
 // shares: [n][t+1][48] compressed (already verified: no subgroup re-check, as
 // in the crate where decrypt consumes parsed shares); idx: [n][t+1] node indices.
-__global__ __launch_bounds__(64) void tdec_combine(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
+TDEC_KERNEL void tdec_combine(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
                                                    const uint32_t* __restrict__ idx, const uint8_t* __restrict__ V,
                                                    const uint64_t* __restrict__ V_off, uint8_t* __restrict__ out,
                                                    int32_t* __restrict__ status, uint32_t* __restrict__ scratch) {
@@ -729,7 +739,7 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
 // 5-level butterfly sums the group and lane 0 hashes and XORs.  Same sum, same
 // error precedence (DuplicateEntry before an undecodable share) as the
 // one-lane-per-ciphertext tdec_combine; 22x the parallelism at N=64 t=21.
-__global__ __launch_bounds__(64) void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
+TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
                                                        const uint32_t* __restrict__ idx,
                                                        const uint8_t* __restrict__ V,
                                                        const uint64_t* __restrict__ V_off,
@@ -788,7 +798,7 @@ __global__ __launch_bounds__(64) void tdec_combine_grp(uint32_t n, uint32_t t, c
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
 //     9 [k]P (64-bit k)  10 P + Q (Jacobian add)
 // Field values cross the boundary as canonical raw limbs (12 u32 LE).
-__global__ __launch_bounds__(64) void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
+TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
                                                 uint32_t* __restrict__ out, uint32_t in_words,
                                                 uint32_t out_words, uint32_t* __restrict__ lines) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
