@@ -104,30 +104,6 @@ def cpu_baseline(n_sample: int):
             "simd": bool(corc.lib().orc_simd_enabled())}
 
 
-def _tdec_cpu_worker(args):
-    """One host process: verify `n` shares + `m` combines with the Python oracle."""
-    n, m = args
-    from oracle import bls12_381 as B
-    from oracle import tcrypto as T
-    g = _tdec_fixture()
-    cts = [T.Ciphertext(B.g1_decompress(bytes.fromhex(c["U"])), bytes.fromhex(c["V"]),
-                        B.g2_decompress(bytes.fromhex(c["W"]))) for c in g["cts"]]
-    pks = [B.g1_decompress(bytes.fromhex(p)) for p in g["pk_shares"]]
-    t0 = time.perf_counter()
-    good = 0
-    for k in range(n):
-        c = k % len(cts)
-        i = (k // len(cts)) % len(pks)
-        h = T.hash_g1_g2(cts[c].U, cts[c].V)  # per share: the crate recomputes it inside the call
-        good += T.verify_decryption_share(pks[i], B.g1_decompress(bytes.fromhex(g["cts"][c]["shares"][i])), cts[c], h)
-    t1 = time.perf_counter()
-    for k in range(m):
-        c = k % len(cts)
-        T.decrypt(g["t"], [(i, B.g1_decompress(bytes.fromhex(x))) for i, x in enumerate(g["cts"][c]["shares"])][
-            : g["t"] + 1], cts[c])
-    return t1 - t0, time.perf_counter() - t1, good
-
-
 def _tdec_fixture():
     # N=64 t=21 key material (BASELINE.json configs[3]): 4 ciphertexts x 64 shares, made
     # by tests/golden/make_golden_tdec.py.  Threshold material cannot be generated on the
@@ -135,21 +111,41 @@ def _tdec_fixture():
     return json.load(open(os.path.join(ROOT, "tests", "golden", "tdec_n64.json")))["scenario"]
 
 
-def cpu_baseline_tdec(per_proc: int = 6):
-    import multiprocessing as mp
-    procs = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
-    procs = max(1, min(procs, os.cpu_count() or 1, 16))
+def cpu_baseline_tdec(n_ct: int = 64, n_comb: int = 256):
+    """The C restatement of threshold_crypto's per-share algorithm
+    (oracle/c/bls_oracle.c: share decode with the crate's [r]P subgroup check,
+    hash_g1_g2 recomputed per call, two full pairings), ciphertexts and key
+    shares decoded once; one contiguous block of shares per host thread."""
+    from oracle import corb
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    threads = max(1, min(threads, os.cpu_count() or 1, 64))
+    g = _tdec_fixture()
+    K, n, t = len(g["cts"]), len(g["pk_shares"]), g["t"]
+    base = [(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in g["cts"]]
+    cts = [base[j % K] for j in range(max(n_ct, n_comb))]
+    U, V, off, W = corb._ct_table(cts[:n_ct])
+    pk = np.frombuffer(b"".join(bytes.fromhex(p) for p in g["pk_shares"]), np.uint8).copy()
+    sh = np.frombuffer(b"".join(bytes.fromhex(g["cts"][j % K]["shares"][i]) for j in range(n_ct) for i in range(n)),
+                       np.uint8).copy()
+    sct = np.repeat(np.arange(n_ct, dtype=np.uint32), n)
+    spk = np.tile(np.arange(n, dtype=np.uint32), n_ct)
     t0 = time.perf_counter()
-    with mp.get_context("spawn").Pool(procs) as pool:
-        res = pool.map(_tdec_cpu_worker, [(per_proc, 1)] * procs)
-    wall = time.perf_counter() - t0
-    tv = max(r[0] for r in res)
-    tc = max(r[1] for r in res)
-    return {"value": procs * per_proc / tv, "unit": "shares/s", "cores": procs, "kind": "port",
-            "combine_cts_per_s": procs / tc,
-            "sample": f"{procs} processes x {per_proc} verify_decryption_share + 1 decrypt (t=21), pure-Python "
-                      f"big-int oracle (oracle/tcrypto.py), {wall:.1f} s wall incl. process start",
-            "all_valid": all(r[2] == per_proc for r in res)}
+    ok = corb.verify_shares_arrays(threads, U, V, off, W, pk, sh, sct, spk)
+    tv = time.perf_counter() - t0
+    _, Vc, offc, _ = corb._ct_table(cts[:n_comb])
+    csh = np.frombuffer(b"".join(bytes.fromhex(g["cts"][j % K]["shares"][i]) for j in range(n_comb)
+                                 for i in range(t + 1)), np.uint8).copy()
+    ix = np.tile(np.arange(t + 1, dtype=np.uint32), n_comb)
+    t0 = time.perf_counter()
+    out, st = corb.decrypt_arrays(threads, t, csh, ix, Vc, offc)
+    tc = time.perf_counter() - t0
+    ref = b"".join(bytes.fromhex(g["cts"][j % K]["plaintext"]) for j in range(n_comb))
+    return {"value": n_ct * n / tv, "unit": "shares/s", "cores": threads, "kind": "port",
+            "combine_cts_per_s": n_comb / tc,
+            "sample": f"{n_ct * n} verify_decryption_share ({n_ct} ciphertexts x {n}) in {tv:.2f} s + {n_comb} "
+                      f"PublicKeySet::decrypt (t={t}) in {tc:.2f} s, oracle/c/bls_oracle.c -O3 (64-bit limbs, "
+                      f"the crate's per-share algorithm), {threads} threads",
+            "all_valid": bool(ok.all()) and bool((st == 0).all()) and out[:len(ref)].tobytes() == ref}
 
 
 def tdec_leg(ctx, dev, n_ct: int, reps: int):

@@ -89,3 +89,62 @@ def test_golden_tdec_reproduces():
         assert (B.g1_compress(ct.U).hex(), ct.V.hex(), B.g2_compress(ct.W).hex()) == (c["U"], c["V"], c["W"])
         assert [B.g1_compress(x).hex() for x in s["shares"][k]] == c["shares"]
         assert s["msgs"][k].hex() == c["plaintext"]
+
+
+# --------------------------------------------------------------------------- C restatement (oracle/c/bls_oracle.c)
+def _fixture(name):
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", name)))["scenario"]
+
+
+@pytest.mark.parametrize("name", ["tdec_golden.json", "tdec_n64.json"])
+def test_c_oracle_matches_fixtures(name):
+    """The C restatement (bench's TDec cpu_baseline) reproduces the committed
+    fixtures: every fixture share verifies, wrong-key / other-ciphertext /
+    undecodable shares do not, ciphertexts verify, plaintexts match."""
+    from oracle import corb
+    g = _fixture(name)
+    cts = [(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in g["cts"]]
+    pk = [bytes.fromhex(p) for p in g["pk_shares"]]
+    n = len(pk)
+    items, expect = [], []
+    for c, ct in enumerate(g["cts"]):
+        for i in list(range(min(n, 6))) + [n - 1]:
+            items.append((bytes.fromhex(ct["shares"][i]), c, i)); expect.append(1)
+        items.append((bytes.fromhex(ct["shares"][1]), c, 2)); expect.append(0)            # wrong key
+        other = g["cts"][(c + 1) % len(g["cts"])]["shares"][0]
+        items.append((bytes.fromhex(other), c, 0)); expect.append(0)                     # another ciphertext's share
+    junk = bytearray(bytes.fromhex(g["cts"][0]["shares"][0])); junk[0] &= 0x7F
+    items.append((bytes(junk), 0, 0)); expect.append(0)                                   # undecodable
+    assert corb.verify_shares(cts, pk, items, threads=4).tolist() == expect
+    assert all(corb.ct_verify(*c) for c in cts)
+    U, V, W = cts[0]
+    assert not corb.ct_verify(U, V + b"x", W)
+    t = g["t"]
+    pts, st = corb.decrypt_batch(t, cts, [[(i, bytes.fromhex(x)) for i, x in enumerate(c["shares"])] for c in g["cts"]])
+    assert st.tolist() == [0] * len(cts)
+    assert [p.hex() for p in pts] == [c["plaintext"] for c in g["cts"]]
+    # shares in a different order / a different subset interpolate to the same plaintext
+    sub = [[(i, bytes.fromhex(c["shares"][i])) for i in reversed(range(n - t - 1, n))] for c in g["cts"]]
+    pts2, st2 = corb.decrypt_batch(t, cts, sub)
+    assert pts2 == pts and st2.tolist() == [0] * len(cts)
+    dup = [[(1, bytes.fromhex(c["shares"][1]))] * (t + 1) for c in g["cts"]]
+    _, st3 = corb.decrypt_batch(t, cts, dup)
+    assert st3.tolist() == [-21] * len(cts)
+
+
+def test_c_oracle_matches_python_oracle_on_edge_points():
+    """Identity share / identity key / out-of-subgroup share: C and Python
+    restatements agree bit for bit (Python oracle on a small scenario)."""
+    from oracle import corb
+    s = scenario()
+    ct = s["cts"][0]
+    cts = [(B.g1_compress(ct.U), ct.V, B.g2_compress(ct.W))]
+    h = T.hash_g1_g2(ct.U, ct.V)
+    pk = [B.g1_compress(p) for p in s["pk_shares"]]
+    x = 5
+    while B.fq_sqrt((x ** 3 + 4) % B.P) is None:
+        x += 1
+    bad_sub = bytearray(x.to_bytes(48, "big")); bad_sub[0] |= 0x80
+    items = [(B.g1_compress(None), 0, 0), (bytes(bad_sub), 0, 1), (B.g1_compress(s["shares"][0][2]), 0, 2)]
+    ref = [int(T.verify_decryption_share(s["pk_shares"][0], None, ct, h)), 0, 1]
+    assert corb.verify_shares(cts, pk, items).tolist() == ref
