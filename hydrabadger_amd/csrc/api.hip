@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -761,6 +762,149 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
         return HBG_OK;
     }
     return finish(c, flags);
+}
+
+// ---------------------------------------------------------------- SURVEY.md §8(f1)/(f2)
+namespace {
+// Host mode: copy `bytes` from the host into scratch slot i; device mode: use as is.
+int stage_in(hbg_ctx* c, uint32_t flags, int slot, const void* src, size_t bytes, const void** out) {
+    if (flags & HBG_DEVICE) {
+        *out = src;
+        return HBG_OK;
+    }
+    void* d;
+    HBG_CHECK(scratch(c, slot, bytes ? bytes : 1, &d));
+    if (bytes) HBG_TRY(hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, c->stream));
+    *out = d;
+    return HBG_OK;
+}
+int stage_out(hbg_ctx* c, uint32_t flags, int slot, void* dst, size_t bytes, void** out) {
+    if (flags & HBG_DEVICE) {
+        *out = dst;
+        return HBG_OK;
+    }
+    return scratch(c, slot, bytes ? bytes : 1, out);
+}
+int drain(hbg_ctx* c, uint32_t flags, std::initializer_list<std::pair<void*, std::pair<const void*, size_t>>> outs) {
+    if (flags & HBG_DEVICE) return finish(c, flags);
+    for (auto& o : outs)
+        if (o.second.second) HBG_TRY(hipMemcpyAsync(o.first, o.second.first, o.second.second, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+bool index_ok(uint32_t flags, const uint32_t* idx, uint64_t n, uint64_t bound) {
+    if (flags & HBG_DEVICE) return true;  // device indices are the caller's contract
+    for (uint64_t k = 0; k < n; ++k)
+        if (idx[k] >= bound) return false;
+    return true;
+}
+constexpr uint64_t kVerifyChunk = 16384;  // messages per bls_verify launch (G2Prepared scratch: 39 KB each)
+}  // namespace
+
+int hbg_bls_sign(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_t n, const uint32_t* msg_sk,
+                 const uint8_t* msg, const uint64_t* msg_off, uint8_t* sig96, uint32_t flags) {
+    if (!c || (n && (!sk32 || !msg_sk || !msg_off || !sig96 || n_sk == 0))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!index_ok(flags, msg_sk, n, n_sk)) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
+    const void *dsk, *dms, *dm, *doff;
+    void* dsig;
+    HBG_CHECK(stage_in(c, flags, 0, sk32, 32ull * n_sk, &dsk));
+    HBG_CHECK(stage_in(c, flags, 1, msg_sk, 4ull * n, &dms));
+    HBG_CHECK(stage_in(c, flags, 2, msg, mlen, &dm));
+    HBG_CHECK(stage_in(c, flags, 3, msg_off, 8ull * (n + 1), &doff));
+    HBG_CHECK(stage_out(c, flags, 4, sig96, 96ull * n, &dsig));
+    HBG_TRY(bls::launch_bls_sign(n, (const uint8_t*)dsk, (const uint32_t*)dms, (const uint8_t*)dm,
+                                 (const uint64_t*)doff, (uint8_t*)dsig, c->stream));
+    return drain(c, flags, {{sig96, {dsig, 96ull * n}}});
+}
+
+int hbg_bls_verify(hbg_ctx* c, uint32_t n_pk, const uint8_t* pk48, uint64_t n, const uint32_t* msg_pk,
+                   const uint8_t* msg, const uint64_t* msg_off, const uint8_t* sig96, uint8_t* ok, uint32_t flags) {
+    if (!c || (n && (!pk48 || !msg_pk || !msg_off || !sig96 || !ok || n_pk == 0))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!index_ok(flags, msg_pk, n, n_pk)) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
+    const void *dpk, *dmp, *dm, *doff, *dsig;
+    void *dok, *paff, *pst, *lines;
+    HBG_CHECK(stage_in(c, flags, 0, pk48, 48ull * n_pk, &dpk));
+    HBG_CHECK(stage_in(c, flags, 1, msg_pk, 4ull * n, &dmp));
+    HBG_CHECK(stage_in(c, flags, 2, msg, mlen, &dm));
+    HBG_CHECK(stage_in(c, flags, 3, msg_off, 8ull * (n + 1), &doff));
+    HBG_CHECK(stage_in(c, flags, 9, sig96, 96ull * n, &dsig));
+    HBG_CHECK(stage_out(c, flags, 4, ok, n, &dok));
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
+    HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
+    const uint64_t chunk = n < kVerifyChunk ? n : kVerifyChunk;
+    HBG_CHECK(scratch(c, 6, 8ull * bls::kLineWordsPerPoint * chunk, &lines));
+    HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+        const uint64_t m = (n - k0) < chunk ? (n - k0) : chunk;
+        HBG_TRY(bls::launch_bls_verify(m, (const uint32_t*)paff, (const int32_t*)pst, (const uint32_t*)dmp + k0,
+                                       (const uint8_t*)dm, (const uint64_t*)doff + k0,
+                                       (const uint8_t*)dsig + 96ull * k0, (uint32_t*)lines, (uint8_t*)dok + k0,
+                                       c->stream));
+    }
+    return drain(c, flags, {{ok, {dok, n}}});
+}
+
+int hbg_tdec_encrypt(hbg_ctx* c, const uint8_t* pk48, uint64_t n, const uint8_t* r32, const uint8_t* msg,
+                     const uint64_t* msg_off, uint8_t* U48, uint8_t* V, uint8_t* W96, uint32_t flags) {
+    if (!c || (n && (!pk48 || !r32 || !msg_off || !U48 || !W96))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
+    if (!(flags & HBG_DEVICE) && mlen && (!msg || !V)) return HBG_E_ARG;
+    const void *dpk, *dr, *dm, *doff;
+    void *dU, *dV, *dW, *paff, *pst;
+    HBG_CHECK(stage_in(c, flags, 0, pk48, 48, &dpk));
+    HBG_CHECK(stage_in(c, flags, 1, r32, 32ull * n, &dr));
+    HBG_CHECK(stage_in(c, flags, 2, msg, mlen, &dm));
+    HBG_CHECK(stage_in(c, flags, 3, msg_off, 8ull * (n + 1), &doff));
+    HBG_CHECK(stage_out(c, flags, 4, U48, 48ull * n, &dU));
+    HBG_CHECK(stage_out(c, flags, 5, V, mlen, &dV));
+    HBG_CHECK(stage_out(c, flags, 9, W96, 96ull * n, &dW));
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords, &paff));
+    HBG_CHECK(scratch(c, 13, 4, &pst));
+    HBG_TRY(bls::launch_tdec_pk_prepare(1, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    int32_t hst = 0;
+    HBG_TRY(hipMemcpyAsync(&hst, pst, 4, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    if (hst != 0) return HBG_E_INVALID_POINT;
+    HBG_TRY(bls::launch_tdec_encrypt(n, (const uint32_t*)paff, (const uint8_t*)dr, (const uint8_t*)dm,
+                                     (const uint64_t*)doff, (uint8_t*)dU, (uint8_t*)dV, (uint8_t*)dW, c->stream));
+    return drain(c, flags, {{U48, {dU, 48ull * n}}, {V, {dV, mlen}}, {W96, {dW, 96ull * n}}});
+}
+
+int hbg_tdec_decrypt_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, uint32_t n_sk, const uint8_t* sk32,
+                            uint64_t n, const uint32_t* share_ct, const uint32_t* share_sk, uint8_t* share48,
+                            int32_t* status, uint32_t flags) {
+    if (!c || (n && (!U48 || !sk32 || !share_ct || !share_sk || !share48 || !status || !n_ct || !n_sk)))
+        return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!index_ok(flags, share_ct, n, n_ct) || !index_ok(flags, share_sk, n, n_sk)) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const void *dU, *dsk, *dsc, *dss;
+    void *dsh, *dst, *uaff, *ust;
+    HBG_CHECK(stage_in(c, flags, 0, U48, 48ull * n_ct, &dU));
+    HBG_CHECK(stage_in(c, flags, 1, sk32, 32ull * n_sk, &dsk));
+    HBG_CHECK(stage_in(c, flags, 2, share_ct, 4ull * n, &dsc));
+    HBG_CHECK(stage_in(c, flags, 3, share_sk, 4ull * n, &dss));
+    HBG_CHECK(stage_out(c, flags, 4, share48, 48ull * n, &dsh));
+    HBG_CHECK(stage_out(c, flags, 5, status, 4ull * n, &dst));
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_ct, &uaff));
+    HBG_CHECK(scratch(c, 13, 4ull * n_ct, &ust));
+    HBG_TRY(bls::launch_tdec_pk_prepare(n_ct, (const uint8_t*)dU, (uint32_t*)uaff, (int32_t*)ust, c->stream));
+    HBG_TRY(bls::launch_tdec_decrypt_share(n, (const uint32_t*)uaff, (const int32_t*)ust, (const uint8_t*)dsk,
+                                           (const uint32_t*)dsc, (const uint32_t*)dss, (uint8_t*)dsh,
+                                           (int32_t*)dst, c->stream));
+    return drain(c, flags, {{share48, {dsh, 48ull * n}}, {status, {dst, 4ull * n}}});
 }
 
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {

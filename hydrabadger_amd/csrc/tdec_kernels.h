@@ -41,6 +41,16 @@ hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, con
                                    const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
                                    CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
                                    hipStream_t st);
+hipError_t launch_bls_sign(uint64_t n, const uint8_t* sk32, const uint32_t* msg_sk, const uint8_t* msg,
+                           const uint64_t* off, uint8_t* sig96, hipStream_t st);
+hipError_t launch_bls_verify(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* msg_pk,
+                             const uint8_t* msg, const uint64_t* off, const uint8_t* sig96, uint32_t* lines,
+                             uint8_t* ok, hipStream_t st);
+hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const uint8_t* r32, const uint8_t* msg,
+                               const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96, hipStream_t st);
+hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const int32_t* u_status, const uint8_t* sk32,
+                                     const uint32_t* share_ct, const uint32_t* share_sk, uint8_t* share48,
+                                     int32_t* status, hipStream_t st);
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,

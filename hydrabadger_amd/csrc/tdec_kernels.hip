@@ -793,6 +793,148 @@ TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
     for (uint64_t b = 0; b < len; ++b) out[off + b] = V[off + b] ^ (uint8_t)(rng.next_u32() & 0xFFu);
 }
 
+// ------------------------------------------------------------------ SURVEY.md §8(f1)/(f2)
+// Wire-message signatures (threshold_crypto SecretKey::sign / PublicKey::verify,
+// reached from hydrabadger lib.rs:405-416 / :434) and the proposer / node side
+// of ThresholdDecrypt (PublicKey::encrypt_with_rng with r explicit,
+// SecretKeyShare::decrypt_share_no_verify).  One work-item per message.
+
+BD void g2_compress(uint8_t* b, const G2A& p) {
+    if (p.inf) {
+        b[0] = 0xC0;
+        for (int i = 1; i < 96; ++i) b[i] = 0;
+        return;
+    }
+    fp_to_be(b, fp_from_mont(p.x.c1));
+    fp_to_be(b + 48, fp_from_mont(p.x.c0));
+    b[0] |= 0x80;
+    if (fp2_gt(p.y, fp2_neg(p.y))) b[0] |= 0x20;
+}
+
+// 32-byte little-endian scalar (an Fr value; [k]P == [k mod r]P for P of order r)
+BD void load_scalar(const uint8_t* p, uint32_t (&k)[8]) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+        k[w] = (uint32_t)p[4 * w] | (uint32_t)p[4 * w + 1] << 8 | (uint32_t)p[4 * w + 2] << 16 |
+               (uint32_t)p[4 * w + 3] << 24;
+}
+
+BD G2 g2_mul_scalar(const Fp2& px, const Fp2& py, const uint32_t (&k)[8]) {
+    G2 r = {fp2_one(), fp2_one(), fp2_zero()};
+    int top = 255;
+    while (top >= 0 && !((k[top >> 5] >> (top & 31)) & 1u)) --top;
+    for (int bit = top; bit >= 0; --bit) {
+        r = g2_dbl(r);
+        if ((k[bit >> 5] >> (bit & 31)) & 1u) r = g2_add_mixed(r, px, py);
+    }
+    return r;
+}
+
+// hash_g2(msg): ChaChaRng seeded with SHA3-256(msg)
+BD G2A hash_g2_msg(const uint8_t* msg, uint32_t len) {
+    uint8_t seed[32];
+    sha3_bytes(msg, len, seed);
+    return hash_g2_from_seed(seed);
+}
+
+// SecretKey::sign(msg) = hash_g2(msg) * sk
+TDEC_KERNEL void bls_sign(uint64_t n, const uint8_t* __restrict__ sk32, const uint32_t* __restrict__ msg_sk,
+                          const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
+                          uint8_t* __restrict__ sig96) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const G2A h = hash_g2_msg(msg + off[k], (uint32_t)(off[k + 1] - off[k]));
+    uint32_t sk[8];
+    load_scalar(sk32 + 32ull * msg_sk[k], sk);
+    G2A s = {fp2_zero(), fp2_zero(), true};
+    if (!h.inf) s = g2_to_affine(g2_mul_scalar(h.x, h.y, sk));
+    g2_compress(sig96 + 96ull * k, s);
+}
+
+// PublicKey::verify(sig, msg): e(pk, hash_g2(msg)) == e(G1, sig); the signature
+// decodes with the crate's subgroup check (SignedWireMessage deserialisation).
+TDEC_KERNEL void bls_verify(uint64_t n, const uint32_t* __restrict__ pk_aff, const int32_t* __restrict__ pk_status,
+                            const uint32_t* __restrict__ msg_pk, const uint8_t* __restrict__ msg,
+                            const uint64_t* __restrict__ off, const uint8_t* __restrict__ sig96,
+                            uint32_t* __restrict__ lines, uint8_t* __restrict__ ok) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t p = msg_pk[k];
+    G2A sig;
+    bool good = pk_status[p] == 0 && g2_decompress(sig96 + 96ull * k, sig, true);
+    if (good) {
+        const G2A h = hash_g2_msg(msg + off[k], (uint32_t)(off[k + 1] - off[k]));
+        uint32_t* lh = lines + k * 2ull * kLineWordsPerPoint;
+        uint32_t* ls = lh + kLineWordsPerPoint;
+        g2_prepare(h.x, h.y, lh);
+        if (!sig.inf) g2_prepare(sig.x, sig.y, ls);
+        const uint32_t* pa = pk_aff + 32ull * p;
+        good = pairing_check2(lh, load_fp(pa), load_fp(pa + 12), pa[24] == 0, ls, fp_const(kG1x),
+                              fp_neg(fp_const(kG1y)), !sig.inf);
+    }
+    ok[k] = good ? 1 : 0;
+}
+
+// PublicKey::encrypt_with_rng with r explicit: U = r G1, V = xor_with_hash(r PK, msg),
+// W = r hash_g1_g2(U, V).  V is written at the message's offsets.
+TDEC_KERNEL void tdec_encrypt(uint64_t n, const uint32_t* __restrict__ pk_aff, const uint8_t* __restrict__ r32,
+                              const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
+                              uint8_t* __restrict__ U48, uint8_t* __restrict__ V, uint8_t* __restrict__ W96) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint32_t r[8];
+    load_scalar(r32 + 32ull * k, r);
+    const G1A u = g1_to_affine(g1_mul_fr(fp_const(kG1x), fp_const(kG1y), r));
+    uint8_t* u48 = U48 + 48ull * k;
+    g1_compress(u48, u);
+    G1A g = {fp_zero(), fp_zero(), true};
+    if (pk_aff[24] == 0) g = g1_to_affine(g1_mul_fr(load_fp(pk_aff), load_fp(pk_aff + 12), r));
+    uint8_t cg[48], seed[32];
+    g1_compress(cg, g);
+    sha3_bytes(cg, 48, seed);
+    ChaChaRng rng;
+    rng.init(seed);
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    for (uint64_t i = 0; i < len; ++i) V[o + i] = msg[o + i] ^ (uint8_t)(rng.next_u32() & 0xFFu);
+    // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
+    uint8_t m[64 + 48];
+    uint32_t mlen;
+    if (len > 64) {
+        sha3_bytes(V + o, (uint32_t)len, m);
+        mlen = 32;
+    } else {
+        for (uint32_t i = 0; i < len; ++i) m[i] = V[o + i];
+        mlen = (uint32_t)len;
+    }
+    for (int i = 0; i < 48; ++i) m[mlen + i] = u48[i];
+    sha3_bytes(m, mlen + 48, seed);
+    const G2A h = hash_g2_from_seed(seed);
+    G2A w = {fp2_zero(), fp2_zero(), true};
+    if (!h.inf) w = g2_to_affine(g2_mul_scalar(h.x, h.y, r));
+    g2_compress(W96 + 96ull * k, w);
+}
+
+// SecretKeyShare::decrypt_share_no_verify: share = U * sk_i (U already decoded:
+// u_aff records from tdec_pk_prepare over the U48 table).
+TDEC_KERNEL void tdec_decrypt_share(uint64_t n, const uint32_t* __restrict__ u_aff,
+                                    const int32_t* __restrict__ u_status, const uint8_t* __restrict__ sk32,
+                                    const uint32_t* __restrict__ share_ct, const uint32_t* __restrict__ share_sk,
+                                    uint8_t* __restrict__ share48, int32_t* __restrict__ status) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t c = share_ct[k];
+    const uint32_t* ua = u_aff + 32ull * c;
+    G1A s = {fp_zero(), fp_zero(), true};
+    const int32_t st = u_status[c];
+    if (st == 0 && ua[24] == 0) {
+        uint32_t sk[8];
+        load_scalar(sk32 + 32ull * share_sk[k], sk);
+        s = g1_to_affine(g1_mul_fr(load_fp(ua), load_fp(ua + 12), sk));
+    }
+    g1_compress(share48 + 48ull * k, s);
+    status[k] = st;
+}
+
 // ------------------------------------------------------------------ unit-test hook
 // op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
@@ -976,6 +1118,33 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
         tdec_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status);
     else
         tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status, scratch);
+    return hipGetLastError();
+}
+static dim3 grid64(uint64_t n) { return dim3((uint32_t)((n + 63) / 64)); }
+hipError_t launch_bls_sign(uint64_t n, const uint8_t* sk32, const uint32_t* msg_sk, const uint8_t* msg,
+                           const uint64_t* off, uint8_t* sig96, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    bls_sign<<<grid64(n), dim3(64), 0, st>>>(n, sk32, msg_sk, msg, off, sig96);
+    return hipGetLastError();
+}
+hipError_t launch_bls_verify(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* msg_pk,
+                             const uint8_t* msg, const uint64_t* off, const uint8_t* sig96, uint32_t* lines,
+                             uint8_t* ok, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    bls_verify<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const uint8_t* r32, const uint8_t* msg,
+                               const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    tdec_encrypt<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, r32, msg, off, U48, V, W96);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const int32_t* u_status, const uint8_t* sk32,
+                                     const uint32_t* share_ct, const uint32_t* share_sk, uint8_t* share48,
+                                     int32_t* status, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    tdec_decrypt_share<<<grid64(n), dim3(64), 0, st>>>(n, u_aff, u_status, sk32, share_ct, share_sk, share48, status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,

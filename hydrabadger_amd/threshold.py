@@ -7,6 +7,10 @@ as hbbft's ``ThresholdDecrypt`` uses it, reached from
   Ciphertext(U, V, W).verify()                         -> hbg_ct_verify          (a12)
   PublicKeyShare.verify_decryption_share(share, ct)    -> hbg_tdec_verify_shares (a14)
   PublicKeySet.decrypt(shares, ct)                     -> hbg_tdec_combine       (a15, a16)
+  PublicKey.encrypt_with_r(msg, r)                     -> hbg_tdec_encrypt       (§8 f1)
+  SecretKey.decrypt_share_no_verify(ct)                -> hbg_tdec_decrypt_shares (§8 f1)
+  SecretKey.sign(msg) / PublicKey.verify(sig, msg)     -> hbg_bls_sign / hbg_bls_verify (§8 f2,
+                                                          src/lib.rs:405-416, :434)
 
 Points are the crate's zcash-compressed bytes (G1 48 B, G2 96 B).  Every
 computation runs in libhbgpu.so on the GPU; there is no CPU fallback.  The
@@ -132,3 +136,109 @@ def test_bls(op: int, inputs: np.ndarray, out_words: int, ctx=None) -> np.ndarra
     check(lib().hbg_test_bls((ctx or default_context()).h, op, n, ptr(inputs), iw, ptr(out), out_words),
           "hbg_test_bls")
     return out
+
+
+# --------------------------------------------------------------------------- SURVEY.md §8(f1), (f2)
+def _scalar_bytes(k) -> bytes:
+    """An Fr scalar as the C ABI's 32-byte little-endian integer (int or bytes)."""
+    if isinstance(k, (bytes, bytearray)):
+        if len(k) != 32:
+            raise ValueError("scalar must be 32 bytes")
+        return bytes(k)
+    return int(k).to_bytes(32, "little")
+
+
+def _msg_table(msgs):
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    buf = np.frombuffer(b"".join(bytes(m) for m in msgs) or b"\0", np.uint8).copy()
+    return buf, off
+
+
+def encrypt_batch(pk48: bytes, msgs: list, rs: list, ctx=None) -> list:
+    """PublicKey::encrypt_with_rng for each (msg, r) with the scalar r explicit
+    (the crate draws it from the caller's RNG)."""
+    n = len(msgs)
+    if n == 0:
+        return []
+    buf, off = _msg_table(msgs)
+    r = np.frombuffer(b"".join(_scalar_bytes(x) for x in rs), np.uint8).copy()
+    pk = np.frombuffer(bytes(pk48), np.uint8).copy()
+    U = np.zeros((n, 48), np.uint8)
+    W = np.zeros((n, 96), np.uint8)
+    V = np.zeros(max(int(off[-1]), 1), np.uint8)
+    check(lib().hbg_tdec_encrypt((ctx or default_context()).h, ptr(pk), n, ptr(r), ptr(buf), ptr(off), ptr(U), ptr(V),
+                                 ptr(W), 0), "PublicKey::encrypt_with_rng")
+    return [Ciphertext(U[k].tobytes(), V[int(off[k]):int(off[k + 1])].tobytes(), W[k].tobytes()) for k in range(n)]
+
+
+def decrypt_shares_batch(cts: list, sks: list, pairs: list, ctx=None):
+    """SecretKeyShare::decrypt_share_no_verify for each (ct index, sk index):
+    returns (share48 list, status array)."""
+    n = len(pairs)
+    if n == 0:
+        return [], np.zeros(0, np.int32)
+    U = np.frombuffer(b"".join(bytes(c.U) for c in cts), np.uint8).copy()
+    sk = np.frombuffer(b"".join(_scalar_bytes(x) for x in sks), np.uint8).copy()
+    sc = np.array([c for c, _ in pairs], np.uint32)
+    ss = np.array([s for _, s in pairs], np.uint32)
+    out = np.zeros((n, 48), np.uint8)
+    st = np.zeros(n, np.int32)
+    check(lib().hbg_tdec_decrypt_shares((ctx or default_context()).h, len(cts), ptr(U), len(sks), ptr(sk), n, ptr(sc),
+                                        ptr(ss), ptr(out), ptr(st), 0), "decrypt_share_no_verify")
+    return [out[k].tobytes() for k in range(n)], st
+
+
+def sign_batch(sks: list, items: list, ctx=None) -> list:
+    """SecretKey::sign: items = [(sk index, msg)] -> 96-B compressed signatures."""
+    n = len(items)
+    if n == 0:
+        return []
+    buf, off = _msg_table([m for _, m in items])
+    sk = np.frombuffer(b"".join(_scalar_bytes(x) for x in sks), np.uint8).copy()
+    ix = np.array([i for i, _ in items], np.uint32)
+    sig = np.zeros((n, 96), np.uint8)
+    check(lib().hbg_bls_sign((ctx or default_context()).h, len(sks), ptr(sk), n, ptr(ix), ptr(buf), ptr(off),
+                             ptr(sig), 0), "SecretKey::sign")
+    return [sig[k].tobytes() for k in range(n)]
+
+
+def verify_sig_batch(pk48s: list, items: list, ctx=None) -> np.ndarray:
+    """PublicKey::verify: items = [(pk index, msg, sig96)] -> ok bits."""
+    n = len(items)
+    if n == 0:
+        return np.zeros(0, np.uint8)
+    buf, off = _msg_table([m for _, m, _ in items])
+    pk = np.frombuffer(b"".join(bytes(p) for p in pk48s), np.uint8).copy()
+    ix = np.array([i for i, _, _ in items], np.uint32)
+    sig = np.frombuffer(b"".join(bytes(s) for _, _, s in items), np.uint8).copy()
+    ok = np.zeros(n, np.uint8)
+    check(lib().hbg_bls_verify((ctx or default_context()).h, len(pk48s), ptr(pk), n, ptr(ix), ptr(buf), ptr(off),
+                               ptr(sig), ptr(ok), 0), "PublicKey::verify")
+    return ok
+
+
+@dataclass
+class SecretKey:
+    """threshold_crypto SecretKey (also SecretKeyShare): an Fr scalar."""
+    scalar: int
+
+    def sign(self, msg: bytes, ctx=None) -> bytes:
+        return sign_batch([self.scalar], [(0, msg)], ctx)[0]
+
+    def decrypt_share_no_verify(self, ct: Ciphertext, ctx=None) -> bytes:
+        shares, st = decrypt_shares_batch([ct], [self.scalar], [(0, 0)], ctx)
+        if st[0] != 0:
+            raise HbgError(int(st[0]), "decrypt_share_no_verify")
+        return shares[0]
+
+
+@dataclass
+class PublicKey:
+    pk: bytes  # G1, 48 B compressed
+
+    def verify(self, sig: bytes, msg: bytes, ctx=None) -> bool:
+        return bool(verify_sig_batch([self.pk], [(0, msg, sig)], ctx)[0])
+
+    def encrypt_with_r(self, msg: bytes, r, ctx=None) -> Ciphertext:
+        return encrypt_batch(self.pk, [msg], [r], ctx)[0]

@@ -170,6 +170,46 @@ int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *sha
                      const uint32_t *share_index, const uint8_t *V, const uint64_t *V_off,
                      uint8_t *plaintext, int32_t *status, uint32_t flags);
 
+/* ---- the proposer / node side of ThresholdDecrypt ------
+ * Scalars cross the boundary as 32-byte little-endian integers (an Fr value:
+ * the crate's FrRepr limbs in order); [k]P == [k mod r]P for the prime-order
+ * points involved, so no range check is needed. */
+
+/* PublicKey::encrypt_with_rng (threshold_crypto) with the randomness explicit:
+ * for message k (msg[msg_off[k] .. msg_off[k+1]]) and scalar r32[k]:
+ * U48[k] = r G1, V (at the message's offsets) = xor_with_hash(r PK, msg),
+ * W96[k] = r hash_g1_g2(U, V).  HBG_E_INVALID_POINT if pk48 does not decode.
+ * Replaces the reference call inside hbbft HoneyBadger::propose
+ * (reached from src/hydrabadger/state.rs:484). */
+int hbg_tdec_encrypt(hbg_ctx *ctx, const uint8_t *pk48, uint64_t n, const uint8_t *r32,
+                     const uint8_t *msg, const uint64_t *msg_off, uint8_t *U48, uint8_t *V,
+                     uint8_t *W96, uint32_t flags);
+
+/* SecretKeyShare::decrypt_share_no_verify for n (ciphertext, key) pairs:
+ * share48[k] = U48[share_ct[k]] * sk32[share_sk[k]].  status[k] = 0, or
+ * HBG_E_INVALID_POINT when that U does not decode (share48[k] is then the
+ * identity encoding).  Reached from hbbft ThresholdDecrypt::start_decryption
+ * (src/hydrabadger/state.rs:487). */
+int hbg_tdec_decrypt_shares(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, uint32_t n_sk,
+                            const uint8_t *sk32, uint64_t n, const uint32_t *share_ct,
+                            const uint32_t *share_sk, uint8_t *share48, int32_t *status,
+                            uint32_t flags);
+
+/* ---- wire-message signatures --------------------------
+ * SecretKey::sign(msg) for n messages: sig96[k] = hash_g2(msg_k) * sk32[msg_sk[k]]
+ * (replaces src/lib.rs:434, WireMessages::start_send). */
+int hbg_bls_sign(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint64_t n,
+                 const uint32_t *msg_sk, const uint8_t *msg, const uint64_t *msg_off,
+                 uint8_t *sig96, uint32_t flags);
+
+/* PublicKey::verify(sig, msg) for n messages: ok[k] = 1 iff pk48[msg_pk[k]]
+ * and sig96[k] decode (the crate's subgroup checks) and
+ * e(pk, hash_g2(msg_k)) == e(G1, sig) (replaces src/lib.rs:405-416,
+ * WireMessages::poll). */
+int hbg_bls_verify(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
+                   const uint32_t *msg_pk, const uint8_t *msg, const uint64_t *msg_off,
+                   const uint8_t *sig96, uint8_t *ok, uint32_t flags);
+
 /* Device-side seeded generator: row k of out gets nbytes of
  * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */
 int hbg_synth_bytes(hbg_ctx *ctx, uint32_t tag, uint64_t first_instance, uint64_t nbytes,

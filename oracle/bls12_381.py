@@ -425,6 +425,9 @@ def g2_decompress(b: bytes):
     if len(b) != 96 or not (b[0] & 0x80):
         raise ValueError("not a compressed G2 point")
     if b[0] & 0x40:
+        # the crate: mask the two top flag bits, everything left must be zero
+        if b[0] & 0x3F or any(b[1:]):
+            raise ValueError("bad infinity encoding")
         return None
     greatest = bool(b[0] & 0x20)
     x1 = int.from_bytes(bytes([b[0] & 0x1F]) + b[1:48], "big")

@@ -463,7 +463,12 @@ static void g1_compress(fp x, fp y, int inf, uint8_t *b) {
 static int g2_decompress(const uint8_t *b, fp2 *x, fp2 *y, int *inf) {
     *inf = 0;
     if (!(b[0] & 0x80)) return 0;
-    if (b[0] & 0x40) { *inf = 1; return 1; }
+    if (b[0] & 0x40) {
+        if (b[0] & 0x3F) return 0;
+        for (int i = 1; i < 96; ++i) if (b[i]) return 0;
+        *inf = 1;
+        return 1;
+    }
     uint64_t c1[6], c0[6];
     if (!be48_to_canon(b, c1, 0x1F)) return 0;
     if (!be48_to_canon(b + 48, c0, 0xFF)) return 0;

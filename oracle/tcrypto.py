@@ -82,6 +82,16 @@ def encrypt(pk, msg: bytes, r: int) -> Ciphertext:
     return Ciphertext(u, v, w)
 
 
+def sign(sk: int, msg: bytes):
+    """SecretKey::sign: hash_g2(msg) * sk (G2)."""
+    return B.g2_mul(hash_g2(msg), sk)
+
+
+def verify(pk, sig, msg: bytes) -> bool:
+    """PublicKey::verify: e(pk, hash_g2(msg)) == e(G1, sig)."""
+    return B.pairing_check([(pk, hash_g2(msg)), (B.g1_neg(B.G1), sig)])
+
+
 def decrypt_share(sk_share: int, ct: Ciphertext):
     """SecretKeyShare::decrypt_share_no_verify: U * sk_i."""
     return B.g1_mul(ct.U, sk_share)

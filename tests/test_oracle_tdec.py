@@ -148,3 +148,27 @@ def test_c_oracle_matches_python_oracle_on_edge_points():
     items = [(B.g1_compress(None), 0, 0), (bytes(bad_sub), 0, 1), (B.g1_compress(s["shares"][0][2]), 0, 2)]
     ref = [int(T.verify_decryption_share(s["pk_shares"][0], None, ct, h)), 0, 1]
     assert corb.verify_shares(cts, pk, items).tolist() == ref
+
+
+def test_sign_verify_oracle_and_bls_golden():
+    """SecretKey::sign / PublicKey::verify restatement (SURVEY.md §8(f2)) and
+    the committed f1/f2 fixture (tests/golden/bls_ops.json) reproduce."""
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bls_ops.json")))
+    sks = [int.from_bytes(bytes.fromhex(k), "little") for k in g["sign"]["sk"]]
+    for it in g["sign"]["items"]:
+        m = bytes.fromhex(it["msg"])
+        sig = T.sign(sks[it["sk"]], m)
+        assert B.g2_compress(sig).hex() == it["sig"]
+        pk = B.g1_mul(B.G1, sks[it["sk"]])
+        assert T.verify(pk, sig, m)
+        assert not T.verify(pk, sig, m + b"!")
+        assert not T.verify(B.g1_mul(B.G1, sks[1 - it["sk"]]), sig, m)
+    pk = B.g1_decompress(bytes.fromhex(g["encrypt"]["pk"]))
+    sk = int.from_bytes(bytes.fromhex(g["encrypt"]["sk"]), "little")
+    for it in g["encrypt"]["items"]:
+        ct = T.encrypt(pk, bytes.fromhex(it["msg"]), int.from_bytes(bytes.fromhex(it["r"]), "little"))
+        assert (B.g1_compress(ct.U).hex(), ct.V.hex(), B.g2_compress(ct.W).hex()) == (it["U"], it["V"], it["W"])
+        assert ct.verify()
+        assert B.g1_compress(T.decrypt_share(sk, ct)).hex() == it["share"]
+        # t = 0 keyset: the single share decrypts
+        assert T.decrypt(0, [(0, T.decrypt_share(sk, ct))], ct) == bytes.fromhex(it["msg"])
