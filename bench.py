@@ -70,6 +70,10 @@ def parse():
                     help="ciphertexts per TDec step (64 shares each, N=64 t=21); 0 disables the TDec leg")
     ap.add_argument("--epoch-nodes", type=int, default=128,
                     help="configs[4]: one N-node network spanning all ranks (RCCL all-gather); 0 disables")
+    ap.add_argument("--wire-msgs", type=int, default=65536,
+                    help="SURVEY.md §8(f2): wire messages signed + verified (0 disables)")
+    ap.add_argument("--f1-cts", type=int, default=16384,
+                    help="SURVEY.md §8(f1): ciphertexts encrypted + x64 decryption shares (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     return ap.parse_args()
@@ -212,6 +216,93 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int):
             "inputs": "tests/golden/tdec_n64.json (4 ciphertexts x 64 shares) replicated, HBM-resident"}
 
 
+def _dev_scalars(n: int, dev, seed: int):
+    """n 32-byte little-endian scalars < 2^254 (< r), device-resident, seeded."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    r = torch.randint(0, 256, (n, 32), dtype=torch.uint8, generator=g)
+    r[:, 31] &= 0x3F
+    return r.to(dev)
+
+
+def wire_leg(ctx, dev, n_msgs: int, msg_len: int, reps: int):
+    """SURVEY.md §8(f2): SecretKey::sign + PublicKey::verify of n_msgs wire
+    messages (64 signing nodes, msg_len-byte messages), device-resident."""
+    from hydrabadger_amd import _lib
+    L = _lib.lib()
+    flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
+    g = torch.Generator(device="cpu").manual_seed(0x5167)
+    msgs = torch.randint(0, 256, (n_msgs * msg_len,), dtype=torch.uint8, generator=g).to(dev)
+    off = (torch.arange(n_msgs + 1, dtype=torch.int64) * msg_len).to(dev)
+    n_keys = 64
+    sk = _dev_scalars(n_keys, dev, 17)
+    from oracle import bls12_381 as B  # checker only: public keys of the 64 signers
+    sk_host = sk.cpu().numpy()
+    pk = torch.from_numpy(np.frombuffer(b"".join(
+        B.g1_compress(B.g1_mul(B.G1, int.from_bytes(sk_host[i].tobytes(), "little"))) for i in range(n_keys)),
+        np.uint8).copy()).to(dev)
+    who = (torch.arange(n_msgs, dtype=torch.int32) % n_keys).to(dev)
+    sig = torch.empty((n_msgs, 96), dtype=torch.uint8, device=dev)
+    ok = torch.empty(n_msgs, dtype=torch.uint8, device=dev)
+
+    def sign():
+        _lib.check(L.hbg_bls_sign(ctx.h, n_keys, sk.data_ptr(), n_msgs, who.data_ptr(), msgs.data_ptr(),
+                                  off.data_ptr(), sig.data_ptr(), flags), "sign")
+
+    def verify():
+        _lib.check(L.hbg_bls_verify(ctx.h, n_keys, pk.data_ptr(), n_msgs, who.data_ptr(), msgs.data_ptr(),
+                                    off.data_ptr(), sig.data_ptr(), ok.data_ptr(), flags), "verify")
+    sign()
+    verify()
+    torch.cuda.synchronize()
+    all_ok = bool(ok.all().item())
+    ms_s = timed(sign, reps)
+    ms_v = timed(verify, reps)
+    return {"workload": f"{n_msgs} wire messages x {msg_len} B, 64 signers (SecretKey::sign / PublicKey::verify)",
+            "sign_per_s": n_msgs / (ms_s * 1e-3), "verify_per_s": n_msgs / (ms_v * 1e-3), "sign_ms": ms_s,
+            "verify_ms": ms_v, "all_verified": all_ok}
+
+
+def tdec_inputs_leg(ctx, dev, n_ct: int, n_nodes: int, reps: int):
+    """SURVEY.md §8(f1): PublicKey::encrypt_with_rng of n_ct 256-B contributions
+    and every node's SecretKeyShare::decrypt_share_no_verify (n_ct x n_nodes)."""
+    from hydrabadger_amd import _lib
+    L = _lib.lib()
+    flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
+    g = _tdec_fixture()
+    pk48 = torch.from_numpy(np.frombuffer(bytes.fromhex(g["cts"][0]["U"]), np.uint8).copy()).to(dev)  # any G1 point
+    msg_len = 256
+    gen = torch.Generator(device="cpu").manual_seed(0x48424247)
+    msgs = torch.randint(0, 256, (n_ct * msg_len,), dtype=torch.uint8, generator=gen).to(dev)
+    off = (torch.arange(n_ct + 1, dtype=torch.int64) * msg_len).to(dev)
+    r = _dev_scalars(n_ct, dev, 23)
+    U = torch.empty((n_ct, 48), dtype=torch.uint8, device=dev)
+    V = torch.empty(n_ct * msg_len, dtype=torch.uint8, device=dev)
+    W = torch.empty((n_ct, 96), dtype=torch.uint8, device=dev)
+    sk = _dev_scalars(n_nodes, dev, 29)
+    n = n_ct * n_nodes
+    sc = torch.arange(n_ct, dtype=torch.int32, device=dev).repeat_interleave(n_nodes)
+    ss = torch.arange(n_nodes, dtype=torch.int32, device=dev).repeat(n_ct)
+    sh = torch.empty((n, 48), dtype=torch.uint8, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def enc():
+        _lib.check(L.hbg_tdec_encrypt(ctx.h, pk48.data_ptr(), n_ct, r.data_ptr(), msgs.data_ptr(), off.data_ptr(),
+                                      U.data_ptr(), V.data_ptr(), W.data_ptr(), flags), "encrypt")
+
+    def shares():
+        _lib.check(L.hbg_tdec_decrypt_shares(ctx.h, n_ct, U.data_ptr(), n_nodes, sk.data_ptr(), n, sc.data_ptr(),
+                                             ss.data_ptr(), sh.data_ptr(), st.data_ptr(), flags), "decrypt_share")
+    enc()
+    shares()
+    torch.cuda.synchronize()
+    ok = bool((st == 0).all().item())
+    ms_e = timed(enc, reps)
+    ms_d = timed(shares, reps)
+    return {"workload": f"{n_ct} x 256-B contributions encrypted, {n_ct} x {n_nodes} decryption shares",
+            "encrypt_per_s": n_ct / (ms_e * 1e-3), "decrypt_shares_per_s": n / (ms_d * 1e-3),
+            "encrypt_ms": ms_e, "decrypt_shares_ms": ms_d, "status_ok": ok}
+
+
 def network_leg(ctx, dev, n_nodes: int, reps: int):
     """configs[4]: the RBC half of one epoch of ONE n_nodes-node network whose
     nodes are split over all ranks (hydrabadger_amd/network.py): encode the
@@ -349,6 +440,12 @@ def main():
         tdec = tdec_leg(ctx, dev, a.tdec_cts, 2)
         tdec["value"] = shard.sum_over_ranks(tdec["value"], dev)  # whole-job shares/s
 
+    wire = tdec_in = None
+    if a.wire_msgs > 0:
+        wire = wire_leg(ctx, dev, a.wire_msgs, 256, 2)
+    if a.f1_cts > 0:
+        tdec_in = tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2)
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_sample)
@@ -368,6 +465,8 @@ def main():
             "shard_bytes_GBps": value * N_NODES * L / PAYLOAD,
             "tdec": tdec,
             "network_epoch": epoch,
+            "wire_signatures": wire,
+            "tdec_inputs": tdec_in,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -798,7 +798,7 @@ bool index_ok(uint32_t flags, const uint32_t* idx, uint64_t n, uint64_t bound) {
         if (idx[k] >= bound) return false;
     return true;
 }
-constexpr uint64_t kVerifyChunk = 16384;  // messages per bls_verify launch (G2Prepared scratch: 39 KB each)
+constexpr uint64_t kVerifyChunk = 131072;  // messages per bls_verify launch (G2Prepared scratch: 39 KB each)
 }  // namespace
 
 int hbg_bls_sign(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_t n, const uint32_t* msg_sk,

@@ -149,43 +149,158 @@ BD Fp rand_fq(ChaChaRng& rng) {
     return fp_zero();
 }
 
-// [k]P for the crate's 508-bit G2 cofactor, P affine (left-to-right double-and-add)
-__device__ __constant__ static const uint32_t gG2Cofactor[16] = {
-    kG2Cofactor[0],  kG2Cofactor[1],  kG2Cofactor[2],  kG2Cofactor[3], kG2Cofactor[4],  kG2Cofactor[5],
-    kG2Cofactor[6],  kG2Cofactor[7],  kG2Cofactor[8],  kG2Cofactor[9], kG2Cofactor[10], kG2Cofactor[11],
-    kG2Cofactor[12], kG2Cofactor[13], kG2Cofactor[14], kG2Cofactor[15]};
+// ---- G2 cofactor clearing (the crate's scale_by_cofactor: [h2]P, h2 the 507-bit
+// G2 cofactor), computed without a 507-bit double-and-add:
+//  * Budroni-Pintore: [h_eff]P = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P) with
+//    h_eff = 3(x^2-1) h2 — an endomorphism identity on all of E'(Fp2);
+//  * [h2]P = [c]([h_eff]P), c = (3(x^2-1))^-1 mod r, because [h2]P has order r
+//    and [r h2] kills E'(Fp2);
+//  * on G2 psi acts as [x], and c = d0(1 + x + 2x^2 + 2x^3) - x^2 + x^4 with
+//    d0 = 0x460055555555aaab, so [c]Q = [d0](1 + psi + 2psi^2 + 2psi^3)Q
+//    + psi^4(Q) - psi^2(Q).
+// 191 G2 doublings + ~45 additions instead of 506 + ~250 (derivation checked
+// against the plain multiplication in tests/test_gpu_tdec.py).
+constexpr uint64_t kCofD0 = 0x460055555555aaabull;
 
-BD G2 g2_scale_by_cofactor(const Fp2& px, const Fp2& py) {
-    G2 r = {px, py, fp2_one()};
-    const int top = 506;  // bit index of the leading one of h2 (507 bits)
-    for (int i = top - 1; i >= 0; --i) {
+BD G2 g2_add_v(const G2& p, const G2& q) {
+    if (fp2_is_zero(p.z)) return q;
+    if (fp2_is_zero(q.z)) return p;
+    const Fp2 Z1Z1 = fp2_sqr(p.z), Z2Z2 = fp2_sqr(q.z);
+    const Fp2 U1 = fp2_mul(p.x, Z2Z2), U2 = fp2_mul(q.x, Z1Z1);
+    const Fp2 S1 = fp2_mul(fp2_mul(p.y, q.z), Z2Z2), S2 = fp2_mul(fp2_mul(q.y, p.z), Z1Z1);
+    const Fp2 H = fp2_sub(U2, U1);
+    const Fp2 rr = fp2_dbl(fp2_sub(S2, S1));
+    if (fp2_is_zero(H)) {
+        if (fp2_is_zero(rr)) return g2_dbl(p);
+        return {fp2_one(), fp2_one(), fp2_zero()};
+    }
+    const Fp2 I = fp2_sqr(fp2_dbl(H));
+    const Fp2 J = fp2_mul(H, I);
+    const Fp2 V = fp2_mul(U1, I);
+    G2 r;
+    r.x = fp2_sub(fp2_sub(fp2_sqr(rr), J), fp2_dbl(V));
+    r.y = fp2_sub(fp2_mul(rr, fp2_sub(V, r.x)), fp2_dbl(fp2_mul(S1, J)));
+    r.z = fp2_mul(fp2_sub(fp2_sub(fp2_sqr(fp2_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+    return r;
+}
+__device__ __noinline__ void g2_add_p(G2* r, const G2* p, const G2* q) { *r = g2_add_v(*p, *q); }
+BD G2 g2_add(const G2& p, const G2& q) {
+    G2 r;
+    g2_add_p(&r, &p, &q);
+    return r;
+}
+BD G2 g2_neg(const G2& p) { return {p.x, fp2_neg(p.y), p.z}; }
+// psi(X, Y, Z) = (conj(X) cx, conj(Y) cy, conj(Z)) in Jacobian coordinates
+BD G2 g2_psi(const G2& p) {
+    return {fp2_mul(fp2_conj(p.x), fp2_const(kPsiX)), fp2_mul(fp2_conj(p.y), fp2_const(kPsiY)), fp2_conj(p.z)};
+}
+// [k]P for Jacobian P (full additions)
+BD G2 g2_mul_u64_jac(const G2& p, uint64_t k) {
+    G2 r = {fp2_one(), fp2_one(), fp2_zero()};
+    for (int i = 63 - __builtin_clzll(k); i >= 0; --i) {
         r = g2_dbl(r);
-        if ((gG2Cofactor[i >> 5] >> (i & 31)) & 1u) r = g2_add_mixed(r, px, py);
+        if ((k >> i) & 1ull) r = g2_add(r, p);
     }
     return r;
 }
 
+BD G2 g2_scale_by_cofactor(const Fp2& px, const Fp2& py) {
+    const G2 P = {px, py, fp2_one()};
+    const G2 nP = g2_neg(P);
+    const G2 t1 = g2_neg(g2_mul_u64(px, py, kBlsX));  // [x]P   (x < 0)
+    const G2 t2 = g2_neg(g2_mul_u64_jac(t1, kBlsX));   // [x^2]P
+    G2 q = g2_add(g2_add(t2, g2_neg(t1)), nP);          // [x^2 - x - 1]P
+    q = g2_add(q, g2_psi(g2_add(t1, nP)));              // + psi([x - 1]P)
+    q = g2_add(q, g2_psi(g2_psi(g2_dbl(P))));           // + psi^2(2P)  = [h_eff]P
+    const G2 s1 = g2_add(q, g2_psi(q));                 // (1 + psi)Q
+    const G2 t = g2_add(s1, g2_dbl(g2_psi(g2_psi(s1)))); // (1 + psi + 2psi^2 + 2psi^3)Q
+    const G2 q2 = g2_psi(g2_psi(q));
+    const G2 q4 = g2_psi(g2_psi(q2));
+    return g2_add(g2_mul_u64_jac(t, kCofD0), g2_add(q4, g2_neg(q2)));
+}
+
+// ---- quadratic-residue test for the try-and-increment search
+// Legendre symbol (a | p) by the binary Jacobi algorithm on the raw limbs.
+// A Montgomery value is a R with R = 2^384 a square, so (aR | p) = (a | p).
+// ~1k limb operations instead of the ~1.4k field multiplications of a failed
+// Fq2::sqrt; returns 1 (square), -1 (non-square) or 0 (a == 0).
+BD int fp_legendre(const Fp& a_in) {
+    Fp a = a_in, n = fp_const(kP);
+    int t = 1;
+    for (int guard = 0; guard < 4096; ++guard) {
+        bool zero = true;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) zero &= a[i] == 0u;
+        if (zero) break;
+        while (a[0] == 0u) {  // whole-limb shift: 32 bits, an even count (no sign change)
+#pragma unroll
+            for (int i = 0; i < 11; ++i) a[i] = a[i + 1];
+            a[11] = 0u;
+        }
+        const uint32_t z = __builtin_ctz(a[0]);
+        if (z) {
+#pragma unroll
+            for (int i = 0; i < 11; ++i) a[i] = __builtin_amdgcn_alignbit(a[i + 1], a[i], z);
+            a[11] >>= z;
+            const uint32_t r8 = n[0] & 7u;
+            if ((z & 1u) && (r8 == 3u || r8 == 5u)) t = -t;
+        }
+        // a odd: make a >= n (swap, quadratic reciprocity), then a -= n (even)
+        uint32_t br = 0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) (void)__builtin_subc(a[i], n[i], br, &br);
+        if (br) {
+            const Fp tmp = a;
+            a = n;
+            n = tmp;
+            if ((a[0] & 3u) == 3u && (n[0] & 3u) == 3u) t = -t;
+        }
+        br = 0;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) a[i] = __builtin_subc(a[i], n[i], br, &br);
+    }
+    bool one = n[0] == 1u;
+#pragma unroll
+    for (int i = 1; i < 12; ++i) one &= n[i] == 0u;
+    return one ? t : 0;
+}
+// a in Fq2 is a square iff its norm a0^2 + a1^2 is a square in Fq (p = 3 mod 4)
+BD bool fp2_is_square(const Fp2& a) { return fp_legendre(fp_add(fp_sqr(a.c0), fp_sqr(a.c1))) >= 0; }
+
 // hash_g2(digest_input) given its 32-byte SHA3 digest as the ChaCha seed.
+// Two phases so a wave clears the cofactor ONCE: lanes find their curve point
+// after a different number of tries (geometric, p = 1/2), so a cofactor
+// multiplication inside the try loop would run once per distinct exit
+// iteration of the wave (~4-6x).  Candidates are screened with the cheap
+// Legendre test; the square root is taken once.  Same point, same RNG stream
+// as the crate.
 BD G2A hash_g2_from_seed(const uint8_t seed[32]) {
     ChaChaRng rng;
     rng.init(seed);
     const Fp2 b2 = {fp_const(kB2), fp_const(kB2)};
     // ~half of all x give a curve point; 128 failures (< 2^-128) never happen —
-    // the bound only guarantees termination.
-    for (int tries = 0; tries < 128; ++tries) {
-        Fp2 x;
-        x.c0 = rand_fq(rng);
-        x.c1 = rand_fq(rng);
-        const bool greatest = (rng.next_u32() & 1u) != 0;
+    // the bounds only guarantee termination.
+    for (int round = 0; round < 4; ++round) {
+        Fp2 x = fp2_zero(), yy = fp2_zero();
+        bool found = false, gr = false;
+        for (int tries = 0; tries < 128 && !found; ++tries) {
+            Fp2 xt;
+            xt.c0 = rand_fq(rng);
+            xt.c1 = rand_fq(rng);
+            const bool greatest = (rng.next_u32() & 1u) != 0;
+            if (!fp2_is_square(fp2_add(fp2_mul(fp2_sqr(xt), xt), b2))) continue;
+            x = xt;
+            gr = greatest;
+            found = true;
+        }
+        if (!found) break;
         bool ok;
-        const Fp2 y = fp2_sqrt(fp2_add(fp2_mul(fp2_sqr(x), x), b2), ok);
-        if (!ok) continue;
+        const Fp2 y = fp2_sqrt(fp2_add(fp2_mul(fp2_sqr(x), x), b2), ok);  // ok: x^3 + b is a square
         const Fp2 ny = fp2_neg(y);
         // the crate: y if (y < negy) ^ greatest else negy
-        const bool y_lt = fp2_gt(ny, y);
-        const Fp2 yy = (y_lt != greatest) ? y : ny;
+        yy = (fp2_gt(ny, y) != gr) ? y : ny;
         const G2A h = g2_to_affine(g2_scale_by_cofactor(x, yy));
-        if (!h.inf) return h;
+        if (!h.inf) return h;  // an identity after clearing: the crate draws again
     }
     return {fp2_zero(), fp2_zero(), true};
 }
@@ -938,7 +1053,7 @@ TDEC_KERNEL void tdec_decrypt_share(uint64_t n, const uint32_t* __restrict__ u_a
 // ------------------------------------------------------------------ unit-test hook
 // op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
-//     9 [k]P (64-bit k)  10 P + Q (Jacobian add)
+//     9 [k]P (64-bit k)  10 P + Q (Jacobian add)  11 Legendre(a), is_square(a + b u)
 // Field values cross the boundary as canonical raw limbs (12 u32 LE).
 TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
                                                 uint32_t* __restrict__ out, uint32_t in_words,
@@ -1008,6 +1123,10 @@ TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
         st(0, r.x);
         st(12, r.y);
         o[24] = r.inf;
+    } else if (op == 11) {
+        // in: a (canonical) -> Legendre symbol of a, and fp2_is_square((a, b))
+        o[0] = (uint32_t)fp_legendre(ld(0));
+        o[1] = fp2_is_square({ld(0), ld(12)}) ? 1u : 0u;
     } else if (op == 8) {
         Fp12 f;
         Fp* c[12] = {&f.c0.c0.c0, &f.c0.c0.c1, &f.c0.c1.c0, &f.c0.c1.c1, &f.c0.c2.c0, &f.c0.c2.c1,

@@ -355,3 +355,33 @@ def test_combine_kernels_interpolate_arbitrary_points(t):
             assert status[c] == _lib.HBG_E_DUPLICATE_ENTRY, c
         else:
             assert status[c] == _lib.HBG_E_INVALID_POINT, c
+
+
+def test_legendre_and_fp2_square_test():
+    """The Jacobi-algorithm quadratic-residue screen of hash_g2's
+    try-and-increment (tdec_kernels.hip fp_legendre / fp2_is_square) agrees
+    with Euler's criterion and with the oracle's Fq2 sqrt."""
+    th = _th()
+    rnd = _rnd(11)
+    vals = [(0, 0), (1, 0), (B.P - 1, 0), (4, 0), (2, 0), (3, 5), (0, 7)] + [(rnd(), rnd()) for _ in range(300)]
+    vals += [((a * a) % B.P, 0) for a in (rnd() for _ in range(20))]
+    out = th.test_bls(11, np.array([limbs(a) + limbs(b) for a, b in vals], np.uint32), 2)
+    for (a, b), o in zip(vals, out):
+        e = pow(a, (B.P - 1) // 2, B.P)
+        leg = 0 if a == 0 else (1 if e == 1 else -1)
+        assert int(np.int32(o[0])) == leg, (a, o[0])
+        assert bool(o[1]) == (B.f2_sqrt((a, b)) is not None)
+
+
+def test_hash_g2_many_seeds_fast_cofactor():
+    """hash_g2 with the Budroni-Pintore + psi-decomposed cofactor clearing and
+    the Legendre screen equals the oracle's plain [h2] multiplication for 48
+    seeds (random and structured)."""
+    th = _th()
+    from oracle.merkle import sha3
+    seeds = [sha3(b"hbg-hash-g2-%d" % i) for i in range(40)] + [bytes([i]) * 32 for i in range(8)]
+    out = th.test_bls(6, np.array([list(np.frombuffer(s, np.uint32)) for s in seeds], np.uint32), 48)
+    for s, o in zip(seeds, out):
+        ref = T._rand_g2(ChaChaRng(s))
+        got = ((from_limbs(o[0:12]), from_limbs(o[12:24])), (from_limbs(o[24:36]), from_limbs(o[36:48])))
+        assert got == ref
