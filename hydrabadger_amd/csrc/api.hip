@@ -561,8 +561,8 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
 
 // Batched PublicKeyShare::verify_decryption_share (tdec_kernels.hip, "batched
 // share verification"): sort shares by ciphertext, cut batches of <= 64,
-// weighted batch sums, then three check rounds (batch, sub-batch of 8, single
-// share).  Host syncs: batch count, round-1 and round-2 list sizes.
+// weighted batch sums, then four check rounds (batch, 16-group, quad, single
+// share).  Host syncs: batch count and the item counts of rounds 1-3.
 // A pk table costs ~2k G1 scalar multiplications to build and saves ~60 G1
 // doublings per share verified under that key.
 constexpr uint64_t kPkTableMinUses = 2048;
@@ -593,44 +593,40 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     void *sums, *lok, *items, *fails;
     HBG_CHECK(scratch(c, 23, (size_t)bls::kBatchSumBytes * nb, &sums));
     HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
-    HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 8 * nb, &items));
+    HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 4 * nb, &items));
     HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
-    uint32_t* counts = (uint32_t*)cnt;  // [0] sub-batch items, [1] failing shares
+    uint32_t* counts = (uint32_t*)cnt;  // [0] 16-group items, [1] failing shares, [2] quad items
+    void* items2;
+    HBG_CHECK(scratch(c, 28, (size_t)bls::kCheckItemBytes * 16 * nb, &items2));
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
-    HBG_TRY(hipMemsetAsync(counts, 0, 8, c->stream));
+    HBG_TRY(hipMemsetAsync(counts, 0, 16, c->stream));
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, (const bls::BatchDesc*)desc, (const uint32_t*)perm, dsh, dsp, dU48,
                                           t.ct_status, paff, pst, tbl, (uint32_t*)sums, (uint8_t*)lok, c->stream));
-    // round 0: every batch sum
+    // round 0: every batch sum; failing batches push their 16-share groups
     HBG_TRY(bls::launch_tdec_batch_check(nb, nullptr, (const bls::BatchDesc*)desc, (const uint32_t*)perm,
                                          (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u, t.coefH, t.coefW, dok,
                                          (bls::CheckItem*)items, counts, (uint32_t*)fails, counts + 1, c->stream));
-    uint32_t h[2];
-    HBG_TRY(hipMemcpyAsync(h, counts, 8, hipMemcpyDeviceToHost, c->stream));
+    uint32_t h[3];
+    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipStreamSynchronize(c->stream));
-    // round 1: sub-batches of failing batches (appends failing shares)
+    // round 1: 16-share groups; failing ones push their quads
     HBG_TRY(bls::launch_tdec_batch_check(h[0], (const bls::CheckItem*)items, (const bls::BatchDesc*)desc,
+                                         (const uint32_t*)perm, (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u,
+                                         t.coefH, t.coefW, dok, (bls::CheckItem*)items2, counts + 2,
+                                         (uint32_t*)fails, counts + 1, c->stream));
+    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    // round 2: quads; failing ones append their shares
+    HBG_TRY(bls::launch_tdec_batch_check(h[2], (const bls::CheckItem*)items2, (const bls::BatchDesc*)desc,
                                          (const uint32_t*)perm, (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u,
                                          t.coefH, t.coefW, dok, nullptr, nullptr, (uint32_t*)fails, counts + 1,
                                          c->stream));
-    HBG_TRY(hipMemcpyAsync(h, counts, 8, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipStreamSynchronize(c->stream));
-    if (getenv("HBG_TDEC_DEBUG")) {
-        fprintf(stderr, "hbg batched verify: n=%u batches=%u sub-items=%u fail-shares=%u\n", n, nb, h[0], h[1]);
-        std::vector<uint32_t> hd(4 * nb), hp(n);
-        std::vector<uint8_t> hl(64 * nb);
-        HBG_TRY(hipMemcpy(hd.data(), desc, 16ull * nb, hipMemcpyDeviceToHost));
-        HBG_TRY(hipMemcpy(hp.data(), perm, 4ull * n, hipMemcpyDeviceToHost));
-        HBG_TRY(hipMemcpy(hl.data(), lok, 64ull * nb, hipMemcpyDeviceToHost));
-        for (uint32_t b = 0; b < nb; ++b) {
-            fprintf(stderr, "  batch %u: start=%u end=%u ct=%u lok=", b, hd[4 * b], hd[4 * b + 1], hd[4 * b + 2]);
-            for (int l = 0; l < 64; ++l) fputc('0' + hl[64 * b + l], stderr);
-            fputc('\n', stderr);
-        }
-        fprintf(stderr, "  perm:");
-        for (uint32_t q = 0; q < n && q < 128; ++q) fprintf(stderr, " %u", hp[q]);
-        fputc('\n', stderr);
-    }
-    // round 2: the shares of failing sub-batches, one by one (the reference's equation)
+    if (getenv("HBG_TDEC_DEBUG"))
+        fprintf(stderr, "hbg batched verify: n=%u batches=%u 16-groups=%u quads=%u fail-shares=%u\n", n, nb, h[0],
+                h[2], h[1]);
+    // round 3: the shares of failing quads, one by one (the reference's equation)
     HBG_TRY(bls::launch_tdec_verify_shares(h[1], dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff, pst, dok,
                                            c->stream, (const uint32_t*)fails));
     return HBG_OK;

@@ -14,7 +14,7 @@ constexpr uint32_t kBatchShares = 64;             // batched verification: share
 
 struct BatchDesc;
 struct CheckItem;
-constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 9 * 2 * 36 * 4;
+constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 21 * 2 * 36 * 4;
 
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,

@@ -465,20 +465,25 @@ TDEC_KERNEL void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ shar
 // e(sum r_i PK_i, W) with 64-bit weights r_i derived from a digest of the
 // whole batch (Bellare-Garay-Rabin small-exponent batch test; a batch holding
 // an invalid share passes with probability <= 2^-63).  A batch is up to 64 shares of one
-// ciphertext, split in 8 sub-batches of 8: round 0 checks every batch sum, a
-// failing batch checks its sub-batch sums (round 1), a failing sub-batch
-// checks its shares one by one with the plain per-share test (round 2,
-// tdec_verify_shares) — so every reported 0 comes from the reference's own
-// per-share equation and every 1 from a passing (sub-)batch.
+// ciphertext, tested as a 4-ary tree: round 0 checks every batch sum, a
+// failing batch checks its four 16-share groups (round 1), a failing group its
+// four quads (round 2), and the shares of a failing quad are checked one by
+// one with the plain per-share test (round 3, tdec_verify_shares) — so every
+// reported 0 comes from the reference's own per-share equation and every 1
+// from a passing (sub)group.
 struct BatchDesc {
     uint32_t start, end, ct, pad;
 };
 struct CheckItem {
-    uint32_t b, node;  // node 0..7: sub-batch, 8: whole batch
+    uint32_t b, node;  // node 0..15: quad, 16..19: 16-share group, 20: whole batch
 };
 constexpr uint32_t kJacWords = 36;                    // Jacobian G1: x, y, z
 constexpr uint32_t kSumWords = 2 * kJacWords;         // (sum r S, sum r PK)
-constexpr uint32_t kBatchSumWords = 9 * kSumWords;    // 8 sub-batch sums + batch sum
+// group-testing tree per batch of 64: nodes 0..15 = quads (4 shares), 16..19 =
+// 16-share groups, 20 = the batch.  At 1 % bad shares this costs ~7.8 pairing
+// checks per 64 shares (9.7 for a 64 -> 8 -> 1 tree, 64 for none).
+constexpr uint32_t kNodes = 21, kNodeBatch = 20, kNode16 = 16;
+constexpr uint32_t kBatchSumWords = kNodes * kSumWords;
 
 __global__ void tdec_iota(uint32_t n, uint32_t* __restrict__ v) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -544,7 +549,7 @@ TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_af
 }
 
 // One 64-lane block per batch: lane = share.  Decompress + subgroup check,
-// weight, and the 8 sub-batch sums + the batch sum by cross-lane butterfly
+// weight, and the quad / 16-group / batch sums by cross-lane butterfly
 // (ds_swizzle/bpermute shuffles: no LDS for the points, so occupancy is set
 // by VGPRs alone).
 TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
@@ -613,14 +618,18 @@ TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
     for (int m = 1; m < 64; m <<= 1) {
         A = g1_add(A, g1_shfl_xor(A, m));
         B = g1_add(B, g1_shfl_xor(B, m));
-        if (m == 4 && (lane & 7u) == 0) {  // sub-batch sums
-            store_jac(out + (lane >> 3) * kSumWords, A);
-            store_jac(out + (lane >> 3) * kSumWords + kJacWords, B);
+        if (m == 2 && (lane & 3u) == 0) {  // quad sums (nodes 0..15)
+            store_jac(out + (lane >> 2) * kSumWords, A);
+            store_jac(out + (lane >> 2) * kSumWords + kJacWords, B);
+        }
+        if (m == 8 && (lane & 15u) == 0) {  // 16-share group sums (nodes 16..19)
+            store_jac(out + (kNode16 + (lane >> 4)) * kSumWords, A);
+            store_jac(out + (kNode16 + (lane >> 4)) * kSumWords + kJacWords, B);
         }
     }
     if (lane == 0) {
-        store_jac(out + 8 * kSumWords, A);
-        store_jac(out + 8 * kSumWords + kJacWords, B);
+        store_jac(out + kNodeBatch * kSumWords, A);
+        store_jac(out + kNodeBatch * kSumWords + kJacWords, B);
     }
 }
 
@@ -638,9 +647,11 @@ TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict_
                                                        uint32_t* __restrict__ fail_n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_items) return;
-    const CheckItem it = items ? items[i] : CheckItem{i, 8u};
+    const CheckItem it = items ? items[i] : CheckItem{i, kNodeBatch};
     const BatchDesc d = desc[it.b];
-    const uint32_t l0 = it.node == 8 ? 0u : 8u * it.node, l1 = it.node == 8 ? kBatchShares : l0 + 8u;
+    const uint32_t size = it.node == kNodeBatch ? 64u : (it.node >= kNode16 ? 16u : 4u);
+    const uint32_t l0 = it.node == kNodeBatch ? 0u : (it.node >= kNode16 ? 16u * (it.node - kNode16) : 4u * it.node);
+    const uint32_t l1 = l0 + size;
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
     bool any = false;
     for (uint32_t l = l0; l < l1; ++l) any |= lok[l] != 0;
@@ -654,11 +665,14 @@ TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict_
     if (pass) {
         for (uint32_t l = l0; l < l1; ++l)
             if (lok[l]) ok[perm[d.start + l]] = 1;
-    } else if (it.node == 8) {
-        for (uint32_t sb = 0; sb < 8; ++sb) {
+    } else if (size > 4u) {  // four children of a quarter the size
+        const uint32_t cs = size / 4u;
+        for (uint32_t c = 0; c < 4; ++c) {
+            const uint32_t c0 = l0 + c * cs;
             bool v = false;
-            for (uint32_t l = 8 * sb; l < 8 * sb + 8; ++l) v |= lok[l] != 0;
-            if (v) next[atomicAdd(next_n, 1u)] = CheckItem{it.b, sb};
+            for (uint32_t l = c0; l < c0 + cs; ++l) v |= lok[l] != 0;
+            const uint32_t node = size == 64u ? kNode16 + c : c0 / 4u;
+            if (v) next[atomicAdd(next_n, 1u)] = CheckItem{it.b, node};
         }
     } else {
         for (uint32_t l = l0; l < l1; ++l)
