@@ -74,6 +74,8 @@ def parse():
                     help="SURVEY.md §8(f2): wire messages signed + verified (0 disables)")
     ap.add_argument("--f1-cts", type=int, default=16384,
                     help="SURVEY.md §8(f1): ciphertexts encrypted + x64 decryption shares (0 disables)")
+    ap.add_argument("--coins", type=int, default=4096,
+                    help="SURVEY.md §8(f3): common coins (x64 signature shares) signed, verified, combined (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     return ap.parse_args()
@@ -303,6 +305,70 @@ def tdec_inputs_leg(ctx, dev, n_ct: int, n_nodes: int, reps: int):
             "encrypt_ms": ms_e, "decrypt_shares_ms": ms_d, "status_ok": ok}
 
 
+def coin_leg(ctx, dev, n_coins: int, n_nodes: int, reps: int):
+    """threshold_sign common coin at N=n_nodes, t=(N-1)/3 —
+    every node signs every coin's nonce (hbg_bls_sign with key shares), all
+    shares verified (hbg_bls_verify with public key shares), first t+1
+    combined + parity (hbg_sig_combine).  Device-resident."""
+    from hydrabadger_amd import _lib
+    from oracle import bls12_381 as B  # checker only: key material of a seeded degree-t polynomial
+    L = _lib.lib()
+    flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
+    t = (n_nodes - 1) // 3
+    rng = np.random.default_rng(0x5167)
+    coeffs = [int.from_bytes(rng.bytes(31), "little") for _ in range(t + 1)]
+    sks = [sum(c * pow(i + 1, j, B.R) for j, c in enumerate(coeffs)) % B.R for i in range(n_nodes)]
+    pk_shares = b"".join(B.g1_compress(B.g1_mul(B.G1, k)) for k in sks)
+    master_pk = B.g1_compress(B.g1_mul(B.G1, coeffs[0]))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    sk = d(np.frombuffer(b"".join(k.to_bytes(32, "little") for k in sks), np.uint8).copy())
+    pk = d(np.frombuffer(pk_shares, np.uint8).copy())
+    mpk = d(np.frombuffer(master_pk, np.uint8).copy())
+    n = n_coins * n_nodes
+    nonce_len = 32
+    docs = torch.from_numpy(np.frombuffer(rng.bytes(n_coins * nonce_len), np.uint8).copy()).to(dev)
+    # message k = coin k // N's nonce, signed by node k % N
+    msgs = docs.view(n_coins, nonce_len).repeat_interleave(n_nodes, dim=0).reshape(-1).contiguous()
+    off = (torch.arange(n + 1, dtype=torch.int64, device=dev) * nonce_len)
+    who = (torch.arange(n, dtype=torch.int32, device=dev) % n_nodes)
+    sig = torch.empty((n, 96), dtype=torch.uint8, device=dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    ix = torch.arange(t + 1, dtype=torch.int32, device=dev).repeat(n_coins)
+    comb_sh = torch.empty((n_coins, t + 1, 96), dtype=torch.uint8, device=dev)
+    out = torch.empty((n_coins, 96), dtype=torch.uint8, device=dev)
+    par = torch.empty(n_coins, dtype=torch.uint8, device=dev)
+    st = torch.empty(n_coins, dtype=torch.int32, device=dev)
+
+    def sign():
+        _lib.check(L.hbg_bls_sign(ctx.h, n_nodes, sk.data_ptr(), n, who.data_ptr(), msgs.data_ptr(), off.data_ptr(),
+                                  sig.data_ptr(), flags), "coin sign")
+
+    def verify():
+        _lib.check(L.hbg_bls_verify(ctx.h, n_nodes, pk.data_ptr(), n, who.data_ptr(), msgs.data_ptr(), off.data_ptr(),
+                                    sig.data_ptr(), ok.data_ptr(), flags), "coin verify")
+
+    def combine():
+        comb_sh.copy_(sig.view(n_coins, n_nodes, 96)[:, : t + 1])
+        _lib.check(L.hbg_sig_combine(ctx.h, t, n_coins, comb_sh.data_ptr(), ix.data_ptr(), out.data_ptr(),
+                                     par.data_ptr(), st.data_ptr(), flags), "coin combine")
+    sign()
+    verify()
+    combine()
+    # the combined signatures verify under the master key
+    ok_m = torch.empty(n_coins, dtype=torch.uint8, device=dev)
+    zeros = torch.zeros(n_coins, dtype=torch.int32, device=dev)
+    off_c = torch.arange(n_coins + 1, dtype=torch.int64, device=dev) * nonce_len
+    _lib.check(L.hbg_bls_verify(ctx.h, 1, mpk.data_ptr(), n_coins, zeros.data_ptr(), docs.data_ptr(), off_c.data_ptr(),
+                                out.data_ptr(), ok_m.data_ptr(), flags), "master verify")
+    torch.cuda.synchronize()
+    good = bool(ok.all().item()) and bool((st == 0).all().item()) and bool(ok_m.all().item())
+    ms_s, ms_v, ms_c = timed(sign, reps), timed(verify, reps), timed(combine, reps)
+    return {"workload": f"{n_coins} coins x {n_nodes} signature shares (t={t})",
+            "share_sign_per_s": n / (ms_s * 1e-3), "share_verify_per_s": n / (ms_v * 1e-3),
+            "combine_coins_per_s": n_coins / (ms_c * 1e-3), "coins_per_s": n_coins / ((ms_s + ms_v + ms_c) * 1e-3),
+            "heads_fraction": float(par.float().mean().item()), "all_ok": good}
+
+
 def network_leg(ctx, dev, n_nodes: int, reps: int):
     """configs[4]: the RBC half of one epoch of ONE n_nodes-node network whose
     nodes are split over all ranks (hydrabadger_amd/network.py): encode the
@@ -445,6 +511,7 @@ def main():
         wire = wire_leg(ctx, dev, a.wire_msgs, 256, 2)
     if a.f1_cts > 0:
         tdec_in = tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2)
+    coin = coin_leg(ctx, dev, a.coins, N_NODES, 2) if a.coins > 0 else None
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -467,6 +534,7 @@ def main():
             "network_epoch": epoch,
             "wire_signatures": wire,
             "tdec_inputs": tdec_in,
+            "coin": coin,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -903,6 +903,26 @@ int hbg_tdec_decrypt_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, uint3
     return drain(c, flags, {{share48, {dsh, 48ull * n}}, {status, {dst, 4ull * n}}});
 }
 
+int hbg_sig_combine(hbg_ctx* c, uint32_t t, uint64_t n, const uint8_t* share96, const uint32_t* share_index,
+                    uint8_t* sig96, uint8_t* parity, int32_t* status, uint32_t flags) {
+    if (!c || (n && (!share96 || !share_index || !sig96 || !parity || !status))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (t + 1 > 32) return HBG_E_ARG;  // one 32-lane group per coin
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t m = (uint64_t)t + 1;
+    const void *dsh, *dix;
+    void *dsig, *dpar, *dst;
+    HBG_CHECK(stage_in(c, flags, 0, share96, 96ull * m * n, &dsh));
+    HBG_CHECK(stage_in(c, flags, 1, share_index, 4ull * m * n, &dix));
+    HBG_CHECK(stage_out(c, flags, 2, sig96, 96ull * n, &dsig));
+    HBG_CHECK(stage_out(c, flags, 3, parity, n, &dpar));
+    HBG_CHECK(stage_out(c, flags, 4, status, 4ull * n, &dst));
+    HBG_TRY(bls::launch_coin_combine((uint32_t)n, t, (const uint8_t*)dsh, (const uint32_t*)dix, (uint8_t*)dsig,
+                                     (uint8_t*)dpar, (int32_t*)dst, c->stream));
+    return drain(c, flags, {{sig96, {dsig, 96ull * n}}, {parity, {dpar, n}}, {status, {dst, 4ull * n}}});
+}
+
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);

@@ -51,6 +51,8 @@ hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const uint8_t
 hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const int32_t* u_status, const uint8_t* sk32,
                                      const uint32_t* share_ct, const uint32_t* share_sk, uint8_t* share48,
                                      int32_t* status, hipStream_t st);
+hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, const uint32_t* idx, uint8_t* sig96,
+                               uint8_t* parity, int32_t* status, hipStream_t st);
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,

@@ -1064,6 +1064,82 @@ TDEC_KERNEL void tdec_decrypt_share(uint64_t n, const uint32_t* __restrict__ u_a
     status[k] = st;
 }
 
+// ------------------------------------------------------------------ SURVEY.md §8(f3)
+// threshold_sign common coin: PublicKeySet::combine_signatures (interpolation
+// at 0 over the first t+1 G2 signature shares) + Signature::parity.  One
+// 32-lane group per coin, lane = share (as tdec_combine_grp, in G2).
+BD G2 g2_shfl_xor(const G2& p, int m) {
+    G2 r;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        r.x.c0[i] = __shfl_xor(p.x.c0[i], m);
+        r.x.c1[i] = __shfl_xor(p.x.c1[i], m);
+        r.y.c0[i] = __shfl_xor(p.y.c0[i], m);
+        r.y.c1[i] = __shfl_xor(p.y.c1[i], m);
+        r.z.c0[i] = __shfl_xor(p.z.c0[i], m);
+        r.z.c1[i] = __shfl_xor(p.z.c1[i], m);
+    }
+    return r;
+}
+
+TDEC_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share96,
+                                  const uint32_t* __restrict__ idx, uint8_t* __restrict__ sig96,
+                                  uint8_t* __restrict__ parity, int32_t* __restrict__ status) {
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+    const uint32_t i = threadIdx.x & 31u, half = threadIdx.x & 32u;
+    const uint32_t m = t + 1;
+    const bool live = g < n;  // no early return: the group shuffles below need every lane
+    const bool act = live && i < m;
+    const uint32_t* ix = idx + (uint64_t)(live ? g : 0) * m;
+    const uint32_t me = act ? ix[i] : 0u;
+    bool dup = false;
+    if (act)
+        for (uint32_t j = i + 1; j < m; ++j) dup |= ix[j] == me;
+    G2A p = {fp2_zero(), fp2_zero(), true};
+    bool bad = false;
+    if (act) bad = !g2_decompress(share96 + ((uint64_t)g * m + i) * 96, p, false);
+    const uint32_t any_dup = (uint32_t)(__ballot(dup) >> half);
+    const uint32_t any_bad = (uint32_t)(__ballot(bad) >> half);
+    const int32_t st = any_dup ? HBG_E_DUPLICATE_ENTRY : (any_bad ? HBG_E_INVALID_POINT : 0);
+    G2 acc = {fp2_one(), fp2_one(), fp2_zero()};
+    if (act && st == 0 && !p.inf) {
+        Fr num = fr_from_u32(1), den = fr_from_u32(1);
+        const Fr xi = fr_from_u32(me + 1);
+        for (uint32_t j = 0; j < m; ++j) {
+            if (j == i) continue;
+            const Fr xj = fr_from_u32(ix[j] + 1);
+            num = fr_mul(num, xj);
+            den = fr_mul(den, fr_sub(xj, xi));
+        }
+        const Fr l = fr_canonical(fr_mul(num, fr_inv(den)));
+        uint32_t lw[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) lw[w] = l.v[w];
+        acc = g2_mul_scalar(p.x, p.y, lw);
+    }
+#pragma unroll 1
+    for (int s = 1; s < 32; s <<= 1) acc = g2_add(acc, g2_shfl_xor(acc, s));
+    if (!live || i != 0) return;
+    status[g] = st;
+    if (st != 0) return;
+    const G2A sig = g2_to_affine(acc);
+    g2_compress(sig96 + 96ull * g, sig);
+    // parity of the ones in the XOR of the 192 uncompressed bytes == parity of
+    // all ones of the encoding (flag byte 0x40 for the identity)
+    uint32_t x = 0;
+    if (sig.inf) {
+        x = 0x40u;
+    } else {
+        const Fp c[4] = {fp_from_mont(sig.x.c0), fp_from_mont(sig.x.c1), fp_from_mont(sig.y.c0),
+                         fp_from_mont(sig.y.c1)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int w = 0; w < 12; ++w) x ^= c[k][w];
+    }
+    parity[g] = (uint8_t)(__builtin_popcount(x) & 1u);
+}
+
 // ------------------------------------------------------------------ unit-test hook
 // op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
@@ -1278,6 +1354,13 @@ hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const in
                                      int32_t* status, hipStream_t st) {
     if (n == 0) return hipSuccess;
     tdec_decrypt_share<<<grid64(n), dim3(64), 0, st>>>(n, u_aff, u_status, sk32, share_ct, share_sk, share48, status);
+    return hipGetLastError();
+}
+hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, const uint32_t* idx, uint8_t* sig96,
+                               uint8_t* parity, int32_t* status, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (t + 1 > 32) return hipErrorInvalidValue;
+    coin_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share96, idx, sig96, parity, status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,

@@ -11,6 +11,7 @@ as hbbft's ``ThresholdDecrypt`` uses it, reached from
   SecretKey.decrypt_share_no_verify(ct)                -> hbg_tdec_decrypt_shares (§8 f1)
   SecretKey.sign(msg) / PublicKey.verify(sig, msg)     -> hbg_bls_sign / hbg_bls_verify (§8 f2,
                                                           src/lib.rs:405-416, :434)
+  combine_signatures(t, shares) (+ Signature::parity)  -> hbg_sig_combine        (§8 f3 coin)
 
 Points are the crate's zcash-compressed bytes (G1 48 B, G2 96 B).  Every
 computation runs in libhbgpu.so on the GPU; there is no CPU fallback.  The
@@ -242,3 +243,37 @@ class PublicKey:
 
     def encrypt_with_r(self, msg: bytes, r, ctx=None) -> Ciphertext:
         return encrypt_batch(self.pk, [msg], [r], ctx)[0]
+
+
+# --------------------------------------------------------------------------- SURVEY.md §8(f3)
+def sig_combine_batch(t: int, shares: list, ctx=None):
+    """PublicKeySet::combine_signatures + Signature::parity for many coins:
+    shares[k] = the first t+1 (node index, 96-B signature share) items.
+    Returns (signatures, parity bits, status array)."""
+    n, m = len(shares), t + 1
+    if n == 0:
+        return [], np.zeros(0, np.uint8), np.zeros(0, np.int32)
+    for s in shares:
+        if len(s) < m:
+            raise NotEnoughShares()
+    sh = np.frombuffer(b"".join(bytes(x) for s in shares for _, x in s[:m]), np.uint8).copy()
+    ix = np.array([[i for i, _ in s[:m]] for s in shares], np.uint32).reshape(n, m)
+    sig = np.zeros((n, 96), np.uint8)
+    par = np.zeros(n, np.uint8)
+    st = np.zeros(n, np.int32)
+    check(lib().hbg_sig_combine((ctx or default_context()).h, t, n, ptr(sh), ptr(ix), ptr(sig), ptr(par), ptr(st), 0),
+          "PublicKeySet::combine_signatures")
+    return [sig[k].tobytes() for k in range(n)], par, st
+
+
+def combine_signatures(t: int, shares, ctx=None) -> tuple:
+    """PublicKeySet::combine_signatures(shares) -> (signature96, parity)."""
+    items = list(shares)
+    if len(items) <= t:
+        raise NotEnoughShares()
+    sigs, par, st = sig_combine_batch(t, [items[: t + 1]], ctx)
+    if st[0] == _lib.HBG_E_DUPLICATE_ENTRY:
+        raise DuplicateEntry(int(st[0]), "PublicKeySet::combine_signatures")
+    if st[0] != 0:
+        raise HbgError(int(st[0]), "PublicKeySet::combine_signatures")
+    return sigs[0], bool(par[0])

@@ -210,6 +210,20 @@ int hbg_bls_verify(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
                    const uint32_t *msg_pk, const uint8_t *msg, const uint64_t *msg_off,
                    const uint8_t *sig96, uint8_t *ok, uint32_t flags);
 
+/* ---- threshold_sign common coin -----------------------
+ * Signature shares are SecretKeyShare::sign(doc) = hbg_bls_sign with the key
+ * shares; PublicKeyShare::verify(share, doc) = hbg_bls_verify with the public
+ * key shares.  This combines them: for coin k, the FIRST t+1 (node index,
+ * share) items in iterator order (share96 [n][t+1][96], share_index
+ * [n][t+1]; x = index + 1) -> sig96[k] = PublicKeySet::combine_signatures,
+ * parity[k] = Signature::parity() (the coin value).  status[k] = 0,
+ * HBG_E_DUPLICATE_ENTRY or HBG_E_INVALID_POINT.  t + 1 <= 32 (HBG_E_ARG
+ * otherwise).  Replaces hbbft ThresholdSign::try_output (reached from
+ * src/hydrabadger/state.rs:487 via BinaryAgreement's coin). */
+int hbg_sig_combine(hbg_ctx *ctx, uint32_t t, uint64_t n, const uint8_t *share96,
+                    const uint32_t *share_index, uint8_t *sig96, uint8_t *parity,
+                    int32_t *status, uint32_t flags);
+
 /* Device-side seeded generator: row k of out gets nbytes of
  * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */
 int hbg_synth_bytes(hbg_ctx *ctx, uint32_t tag, uint64_t first_instance, uint64_t nbytes,

@@ -134,6 +134,54 @@ def interpolate(t: int, items: list):
     return acc
 
 
+def interpolate_g2(t: int, items: list):
+    """``interpolate`` over G2 samples (PublicKeySet::combine_signatures):
+    first t+1 (index, G2) items, x = index+1, value at 0."""
+    samples = [(i + 1, s) for i, s in items[: t + 1]]
+    if len(samples) <= t:
+        raise NotEnoughShares()
+    xs = [x for x, _ in samples]
+    if len(set(xs)) != len(xs):
+        raise DuplicateEntry()
+    if t == 0:
+        return samples[0][1]
+    acc = None
+    for x, s in samples:
+        num, den = 1, 1
+        for x0 in xs:
+            if x0 != x:
+                num = num * x0 % B.R
+                den = den * (x0 - x) % B.R
+        acc = B.g2_add(acc, B.g2_mul(s, num * pow(den, -1, B.R) % B.R))
+    return acc
+
+
+def combine_signatures(t: int, shares: list):
+    """PublicKeySet::combine_signatures(shares): shares = [(index, G2 sig share)]."""
+    return interpolate_g2(t, shares)
+
+
+def g2_uncompressed(pt) -> bytes:
+    """zcash uncompressed G2 (192 B): x.c1 || x.c0 || y.c1 || y.c0 big-endian,
+    flag bit 6 for the identity (bit 7, 'compressed', clear)."""
+    if pt is None:
+        out = bytearray(192)
+        out[0] = 0x40
+        return bytes(out)
+    (x0, x1), (y0, y1) = pt
+    return b"".join(v.to_bytes(48, "big") for v in (x1, x0, y1, y0))
+
+
+def sig_parity(sig) -> bool:
+    """Signature::parity (threshold_crypto [EXT], version-dependent — parity
+    unpinned): XOR of all bytes of the uncompressed encoding, then the parity
+    of that byte's number of ones — the hbbft common-coin bit."""
+    x = 0
+    for b in g2_uncompressed(sig):
+        x ^= b
+    return bin(x).count("1") % 2 == 1
+
+
 def decrypt(t: int, shares: list, ct: Ciphertext) -> bytes:
     """PublicKeySet::decrypt(shares, ct): shares = [(index, G1)] in iterator order."""
     g = interpolate(t, shares)

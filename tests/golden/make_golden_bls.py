@@ -38,7 +38,21 @@ def main():
         enc["items"].append({"r": le(r), "msg": m.hex(), "U": B.g1_compress(ct.U).hex(), "V": ct.V.hex(),
                              "W": B.g2_compress(ct.W).hex(),
                              "share": B.g1_compress(T.decrypt_share(pk_sk, ct)).hex()})
-    out = {"generator": "tests/golden/make_golden_bls.py", "sign": sign, "encrypt": enc}
+    # §8(f3) common coin at N=7 t=2: signature shares of a nonce, their
+    # combination (== the master key's signature) and its parity
+    from tests.tdec_fixtures import scenario
+    s = scenario()
+    ks, t, n = s["ks"], s["t"], len(s["pk_shares"])
+    coins = []
+    for nonce in (b"coin epoch 0 round 0", b"coin epoch 7 round 3"):
+        shares = [T.sign(ks.secret_key_share(i), nonce) for i in range(n)]
+        sig = T.combine_signatures(t, [(i, shares[i]) for i in range(n)][1:1 + t + 1])
+        assert sig == T.sign(ks.coeffs[0], nonce)
+        coins.append({"doc": nonce.hex(), "shares": [B.g2_compress(x).hex() for x in shares],
+                      "sig": B.g2_compress(sig).hex(), "parity": T.sig_parity(sig)})
+    coin = {"t": t, "pk": B.g1_compress(ks.public_key()).hex(),
+            "pk_shares": [B.g1_compress(p).hex() for p in s["pk_shares"]], "coins": coins}
+    out = {"generator": "tests/golden/make_golden_bls.py", "sign": sign, "encrypt": enc, "coin": coin}
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "bls_ops.json"), "w") as f:
         json.dump(out, f, indent=1)
 

@@ -121,3 +121,57 @@ def test_epoch_round_trip_on_device():
     assert ok.all()
     pts, st = th.combine_batch(t, cts, [[(i, shares[c * n + i]) for i in range(n)][:t + 1] for c in range(len(cts))])
     assert st.tolist() == [0] * len(cts) and pts == msgs
+
+
+def test_coin_sign_verify_combine_matches_fixture():
+    """§8(f3): signature shares (hbg_bls_sign with key shares), share
+    verification (hbg_bls_verify with public key shares) and
+    combine_signatures + parity (hbg_sig_combine) reproduce the fixture."""
+    th = _th()
+    c = G["coin"]
+    t = c["t"]
+    s = scenario()
+    ks, n = s["ks"], len(s["pk_shares"])
+    sks = [ks.secret_key_share(i) for i in range(n)]
+    pks = [bytes.fromhex(p) for p in c["pk_shares"]]
+    for coin in c["coins"]:
+        doc = bytes.fromhex(coin["doc"])
+        shares = th.sign_batch(sks, [(i, doc) for i in range(n)])
+        assert [x.hex() for x in shares] == coin["shares"]
+        items = [(i, doc, shares[i]) for i in range(n)] + [(3, doc, shares[4]), (2, doc + b"x", shares[2])]
+        assert th.verify_sig_batch(pks, items).tolist() == [1] * n + [0, 0]
+        for lo in (0, 1, n - t - 1):
+            sig, par = th.combine_signatures(t, [(i, shares[i]) for i in range(lo, lo + t + 1)])
+            assert sig.hex() == coin["sig"] and par == coin["parity"]
+        with pytest.raises(th.DuplicateEntry):
+            th.combine_signatures(t, [(1, shares[1])] * (t + 1))
+        assert th.PublicKey(bytes.fromhex(c["pk"])).verify(bytes.fromhex(coin["sig"]), doc)
+
+
+@pytest.mark.parametrize("t", [0, 3, 21, 31])
+def test_coin_combine_arbitrary_points(t):
+    """hbg_sig_combine over arbitrary G2 points (interpolation does not need
+    valid shares), odd coin count, identity shares, sparse shuffled indices,
+    and an undecodable share — against the oracle's interpolate_g2 + parity."""
+    th = _th()
+    from hydrabadger_amd import _lib
+    rng = random.Random(2000 + t)
+    coins, expect = [], []
+    for k in range(3):
+        ids = rng.sample(range(100), t + 1)
+        pts = [None if (k == 1 and j == 0) else B.g2_mul(B.G2, rng.randrange(1, B.R)) for j in range(t + 1)]
+        items = [(i, B.g2_compress(p)) for i, p in zip(ids, pts)]
+        if k == 2:
+            junk = bytearray(items[-1][1]); junk[0] &= 0x7F
+            items[-1] = (items[-1][0], bytes(junk))
+            expect.append(None)
+        else:
+            sig = T.combine_signatures(t, list(zip(ids, pts)))
+            expect.append((B.g2_compress(sig), T.sig_parity(sig)))
+        coins.append(items)
+    sigs, par, st = th.sig_combine_batch(t, coins)
+    for k, e in enumerate(expect):
+        if e is None:
+            assert st[k] == _lib.HBG_E_INVALID_POINT
+        else:
+            assert st[k] == 0 and sigs[k] == e[0] and bool(par[k]) == e[1], k

@@ -172,3 +172,21 @@ def test_sign_verify_oracle_and_bls_golden():
         assert B.g1_compress(T.decrypt_share(sk, ct)).hex() == it["share"]
         # t = 0 keyset: the single share decrypts
         assert T.decrypt(0, [(0, T.decrypt_share(sk, ct))], ct) == bytes.fromhex(it["msg"])
+
+
+def test_coin_oracle_fixture():
+    """§8(f3) common coin: signature shares interpolate to the master key's
+    signature for any t+1 subset; parity recorded in the fixture."""
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bls_ops.json")))["coin"]
+    t = g["t"]
+    pk = B.g1_decompress(bytes.fromhex(g["pk"]))
+    for c in g["coins"]:
+        doc = bytes.fromhex(c["doc"])
+        shares = [B.g2_decompress(bytes.fromhex(x)) for x in c["shares"]]
+        for lo in (0, len(shares) - t - 1):
+            sig = T.combine_signatures(t, [(i, shares[i]) for i in range(lo, lo + t + 1)])
+            assert B.g2_compress(sig).hex() == c["sig"]
+        assert T.sig_parity(B.g2_decompress(bytes.fromhex(c["sig"]))) == c["parity"]
+        assert T.verify(pk, B.g2_decompress(bytes.fromhex(c["sig"])), doc)
+        pks = [B.g1_decompress(bytes.fromhex(p)) for p in g["pk_shares"]]
+        assert T.verify(pks[3], shares[3], doc) and not T.verify(pks[3], shares[4], doc)
