@@ -486,14 +486,17 @@ __global__ void rbc_glue_status(const uint8_t* __restrict__ shards, uint64_t S, 
     status[k] = good ? HBG_DECODE_OK : HBG_DECODE_NONE;
 }
 
-// payload byte q = value byte q+4; thread per output word.
+// payload byte q = value byte q+4 of the concatenated data rows; one thread per
+// 16 output bytes: 5 aligned dword loads + 4 v_alignbyte, one 16-B store when the
+// destination allows it (byte loop only where a window crosses a row end or
+// the payload end).
 __global__ __launch_bounds__(256) void rbc_glue_copy(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                      uint32_t N, uint64_t n, uint32_t blocks_per_inst,
                                                      const uint64_t* __restrict__ plen,
                                                      const uint8_t* __restrict__ status, uint8_t* __restrict__ out,
                                                      uint64_t ostride) {
     const uint64_t inst = blockIdx.x / blocks_per_inst;
-    const uint64_t q = ((uint64_t)(blockIdx.x % blocks_per_inst) * 256 + threadIdx.x) * 4;
+    const uint64_t q = ((uint64_t)(blockIdx.x % blocks_per_inst) * 256 + threadIdx.x) * 16;
     if (inst >= n || status[inst] != HBG_DECODE_OK) return;
     const uint64_t len = plen[inst];
     if (q >= len) return;
@@ -501,26 +504,33 @@ __global__ __launch_bounds__(256) void rbc_glue_copy(const uint8_t* __restrict__
     const uint32_t Lw = (uint32_t)L;
     const uint32_t x = (uint32_t)(q + 4);
     const uint32_t r = x / Lw, c = x - r * Lw;
-    uint32_t w;
-    if (c + 4 <= Lw) {
-        const uint8_t* rowp = base + (uint64_t)r * S;
-        const uint32_t* pw = reinterpret_cast<const uint32_t*>(rowp) + (c >> 2);
-        const uint32_t s = c & 3;
-        const uint32_t w0 = pw[0];
-        const uint32_t w1 = s ? pw[1] : 0u;
-        w = __builtin_amdgcn_alignbyte(w1, w0, s);
-    } else {
-        w = 0;
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t xb = x + b, rb = xb / Lw, cb = xb - rb * Lw;
-            w |= (uint32_t)base[(uint64_t)rb * S + cb] << (8 * b);
-        }
-    }
     uint8_t* dst = out + inst * ostride + q;
-    if (q + 4 <= len) {
-        *reinterpret_cast<uint32_t*>(dst) = w;  // ostride % 4 == 0
-    } else {
-        for (uint64_t b = 0; q + b < len; ++b) dst[b] = (uint8_t)(w >> (8 * b));
+    if (c + 16 <= Lw && q + 16 <= len) {
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(base + (uint64_t)r * S) + (c >> 2);
+        const uint32_t s = c & 3;
+        uint32_t v[5];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = pw[i];
+        v[4] = s ? pw[4] : 0u;  // pw[4] lies inside the row (c + 16 <= L) when s != 0
+        uint4 w;
+        w.x = __builtin_amdgcn_alignbyte(v[1], v[0], s);
+        w.y = __builtin_amdgcn_alignbyte(v[2], v[1], s);
+        w.z = __builtin_amdgcn_alignbyte(v[3], v[2], s);
+        w.w = __builtin_amdgcn_alignbyte(v[4], v[3], s);
+        if (((uintptr_t)dst & 15u) == 0) {
+            *reinterpret_cast<uint4*>(dst) = w;
+        } else {  // ostride % 4 == 0
+            uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+            d4[0] = w.x;
+            d4[1] = w.y;
+            d4[2] = w.z;
+            d4[3] = w.w;
+        }
+        return;
+    }
+    for (uint32_t b = 0; b < 16 && q + b < len; ++b) {
+        const uint32_t xb = x + b, rb = xb / Lw, cb = xb - rb * Lw;
+        dst[b] = base[(uint64_t)rb * S + cb];
     }
 }
 
@@ -647,7 +657,7 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t maxlen = (uint64_t)D * L;
-    const uint32_t bpi = (uint32_t)(((maxlen + 3) / 4 + 255) / 256);
+    const uint32_t bpi = (uint32_t)(((maxlen + 15) / 16 + 255) / 256);
     rbc_glue_copy<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, plen, status, out,
                                                                     ostride);
     return hipGetLastError();
