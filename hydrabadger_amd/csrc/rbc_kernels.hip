@@ -245,6 +245,84 @@ __global__ __launch_bounds__(256) void rs_code_generic(uint8_t* __restrict__ sha
     }
 }
 
+// Register-table variant: the 16 + 16 split-nibble combinations of each data
+// word stay in VGPRs and the wave-uniform coefficient (decoded with SALU from
+// the plan's offsets) selects them by M0-relative register addressing
+// (v_movrels): no LDS traffic, 2 selects + 1 v_bitop3 per MAC-word.
+#ifndef HBG_MOVREL_SPLIT
+#define HBG_MOVREL_SPLIT 16
+#endif
+constexpr int kMovrelSplit = HBG_MOVREL_SPLIT;
+__global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+                                                      uint32_t N, uint32_t D, uint64_t n,
+                                                      uint32_t blocks_per_inst, const uint8_t* __restrict__ plans,
+                                                      uint64_t plan_stride) {
+    typedef const __attribute__((address_space(4))) uint32_t* cu32;  // scalar (SMEM) loads
+    const uint64_t inst = blockIdx.x / blocks_per_inst;
+    const uint32_t p = (blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
+    if (inst >= n) return;
+    const uint32_t Q = N - D, qp = plan_qpad(Q);
+    const uint8_t* pbase = plans + inst * plan_stride;
+    const CodePlan* plan = reinterpret_cast<const CodePlan*>(pbase);
+    if (plan->status != 0) return;
+    const uint32_t n_out = plan->n_out;
+    const bool active = 4 * (uint64_t)p < L;
+    const cu32 offs = (cu32)(pbase + plan_offs_at(D, Q));
+    uint8_t* base = shards + inst * (uint64_t)N * S;
+    extern __shared__ uint32_t gtab[];
+    uint32_t* tab = gtab + (threadIdx.x >> 6) * (32 * 64) + (threadIdx.x & 63);  // entry e at tab[64 e]
+    const uint32_t tab_addr = (uint32_t)(uintptr_t)tab;                             // LDS byte address
+    tab[0] = 0u;
+    tab[16 * 64] = 0u;
+    for (uint32_t o0 = 0; o0 < n_out; o0 += kGenericTile) {
+        uint32_t acc[kGenericTile];
+#pragma unroll
+        for (int o = 0; o < (int)kGenericTile; ++o) acc[o] = 0u;
+        const uint32_t cnt = (n_out - o0) < (uint32_t)kGenericTile ? (n_out - o0) : (uint32_t)kGenericTile;
+        for (uint32_t j = 0; j < D; ++j) {
+            const uint32_t w =
+                active ? reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p] : 0u;
+            const NibPair T = nib_tables(w);
+            typedef uint32_t v16 __attribute__((ext_vector_type(16)));
+            v16 tl, th;  // vector values: a dynamic uniform index lowers to v_movrels
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                tl[e] = T.lo.t[e];
+                th[e] = T.hi.t[e];
+            }
+            if (kMovrelSplit < (int)kGenericTile) {
+#pragma unroll
+                for (int e = 1; e < 16; ++e) {
+                    tab[64 * e] = T.lo.t[e];
+                    tab[64 * (16 + e)] = T.hi.t[e];
+                }
+            }
+            const cu32 oj = offs + 2 * ((uint64_t)j * qp + o0);
+            typedef const __attribute__((address_space(3))) uint32_t* lds32;
+            // offsets are LDS byte offsets 256 * entry (rs_plan); padded rows
+            // (o >= cnt) point at entry 0 of both tables, i.e. zero.  Rows below
+            // kMovrelSplit select from registers (SALU + v_movrels), the rest read
+            // the LDS copy: the two pipes run side by side.
+#pragma unroll
+            for (int o = 0; o < (int)kGenericTile; ++o) {
+                if (o < kMovrelSplit) {
+                    const uint32_t lo = oj[2 * o] >> 8, hi = (oj[2 * o + 1] >> 8) - 16u;
+                    acc[o] = xor3u(acc[o], tl[lo & 15u], th[hi & 15u]);
+                } else {
+                    acc[o] = xor3u(acc[o], *(lds32)(uintptr_t)(tab_addr + oj[2 * o]),
+                                   *(lds32)(uintptr_t)(tab_addr + oj[2 * o + 1]));
+                }
+            }
+        }
+        if (active) {
+#pragma unroll
+            for (int o = 0; o < (int)kGenericTile; ++o)
+                if ((uint32_t)o < cnt)
+                    reinterpret_cast<uint32_t*>(base + (uint64_t)plan->out_idx[o0 + o] * S)[p] = acc[o];
+        }
+    }
+}
+
 // Per-instance reconstruct plan (rse reconstruct_internal, restated):
 // rows_used = first D present rows in index order; dec = inv(M[rows_used]);
 // for every missing row r: coef[r] = M[r] * dec (so one pass rebuilds missing
@@ -608,6 +686,15 @@ hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N,
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    static const int impl = [] {
+        const char* e = getenv("HBG_GENERIC_IMPL");
+        return e ? atoi(e) : 1;
+    }();
+    if (impl == 1) {
+        rs_code_movrel<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
+                                                                                plan_stride);
+        return hipGetLastError();
+    }
     rs_code_generic<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
                                                                       plan_stride);
     return hipGetLastError();
