@@ -74,7 +74,7 @@ def parse():
                     help="SURVEY.md §8(f2): wire messages signed + verified (0 disables)")
     ap.add_argument("--f1-cts", type=int, default=16384,
                     help="SURVEY.md §8(f1): ciphertexts encrypted + x64 decryption shares (0 disables)")
-    ap.add_argument("--coins", type=int, default=4096,
+    ap.add_argument("--coins", type=int, default=16384,
                     help="SURVEY.md §8(f3): common coins (x64 signature shares) signed, verified, combined (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
@@ -308,8 +308,10 @@ def tdec_inputs_leg(ctx, dev, n_ct: int, n_nodes: int, reps: int):
 def coin_leg(ctx, dev, n_coins: int, n_nodes: int, reps: int):
     """threshold_sign common coin at N=n_nodes, t=(N-1)/3 —
     every node signs every coin's nonce (hbg_bls_sign with key shares), all
-    shares verified (hbg_bls_verify with public key shares), first t+1
-    combined + parity (hbg_sig_combine).  Device-resident."""
+    shares verified with 1 % of them replaced by another node's share
+    (hbg_sig_verify_shares: hash_g2 once per coin, weighted batches; the
+    per-share hbg_bls_verify timed beside it), first t+1 combined + parity
+    (hbg_sig_combine).  Device-resident."""
     from hydrabadger_amd import _lib
     from oracle import bls12_381 as B  # checker only: key material of a seeded degree-t polynomial
     L = _lib.lib()
@@ -343,28 +345,45 @@ def coin_leg(ctx, dev, n_coins: int, n_nodes: int, reps: int):
         _lib.check(L.hbg_bls_sign(ctx.h, n_nodes, sk.data_ptr(), n, who.data_ptr(), msgs.data_ptr(), off.data_ptr(),
                                   sig.data_ptr(), flags), "coin sign")
 
+    # 1 % of the verified shares claim another node's share of the same coin
+    bad = torch.from_numpy(rng.random(n) < 0.01).to(dev)
+    sig_v = torch.empty_like(sig)
+    share_doc = (torch.arange(n, dtype=torch.int32, device=dev) // n_nodes)
+    off_c = torch.arange(n_coins + 1, dtype=torch.int64, device=dev) * nonce_len
+    ok1 = torch.empty(n, dtype=torch.uint8, device=dev)
+
     def verify():
+        _lib.check(L.hbg_sig_verify_shares(ctx.h, n_coins, docs.data_ptr(), off_c.data_ptr(), n_nodes, pk.data_ptr(),
+                                           n, sig_v.data_ptr(), share_doc.data_ptr(), who.data_ptr(), ok.data_ptr(),
+                                           flags), "coin verify")
+
+    def verify_per_share():
         _lib.check(L.hbg_bls_verify(ctx.h, n_nodes, pk.data_ptr(), n, who.data_ptr(), msgs.data_ptr(), off.data_ptr(),
-                                    sig.data_ptr(), ok.data_ptr(), flags), "coin verify")
+                                    sig_v.data_ptr(), ok1.data_ptr(), flags), "coin verify per share")
 
     def combine():
         comb_sh.copy_(sig.view(n_coins, n_nodes, 96)[:, : t + 1])
         _lib.check(L.hbg_sig_combine(ctx.h, t, n_coins, comb_sh.data_ptr(), ix.data_ptr(), out.data_ptr(),
                                      par.data_ptr(), st.data_ptr(), flags), "coin combine")
     sign()
+    sh = sig.view(n_coins, n_nodes, 96)
+    sig_v.copy_(torch.where(bad.view(n_coins, n_nodes, 1), sh.roll(1, dims=1), sh).view(n, 96))
     verify()
+    verify_per_share()
     combine()
     # the combined signatures verify under the master key
     ok_m = torch.empty(n_coins, dtype=torch.uint8, device=dev)
     zeros = torch.zeros(n_coins, dtype=torch.int32, device=dev)
-    off_c = torch.arange(n_coins + 1, dtype=torch.int64, device=dev) * nonce_len
     _lib.check(L.hbg_bls_verify(ctx.h, 1, mpk.data_ptr(), n_coins, zeros.data_ptr(), docs.data_ptr(), off_c.data_ptr(),
                                 out.data_ptr(), ok_m.data_ptr(), flags), "master verify")
     torch.cuda.synchronize()
-    good = bool(ok.all().item()) and bool((st == 0).all().item()) and bool(ok_m.all().item())
+    good = (bool(torch.equal(ok, (~bad).to(torch.uint8))) and bool(torch.equal(ok1, ok))
+            and bool((st == 0).all().item()) and bool(ok_m.all().item()))
     ms_s, ms_v, ms_c = timed(sign, reps), timed(verify, reps), timed(combine, reps)
-    return {"workload": f"{n_coins} coins x {n_nodes} signature shares (t={t})",
+    ms_v1 = timed(verify_per_share, 1)
+    return {"workload": f"{n_coins} coins x {n_nodes} signature shares (t={t}), 1 % of the verified shares wrong",
             "share_sign_per_s": n / (ms_s * 1e-3), "share_verify_per_s": n / (ms_v * 1e-3),
+            "share_verify_per_share_path_per_s": n / (ms_v1 * 1e-3), "wrong_shares": int(bad.sum().item()),
             "combine_coins_per_s": n_coins / (ms_c * 1e-3), "coins_per_s": n_coins / ((ms_s + ms_v + ms_c) * 1e-3),
             "heads_fraction": float(par.float().mean().item()), "all_ok": good}
 

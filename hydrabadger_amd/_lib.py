@@ -67,6 +67,7 @@ SIGNATURES = {
     "hbg_bls_sign": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u32]),
     "hbg_bls_verify": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u8p, _u32]),
     "hbg_sig_combine": (_i, [_vp, _u32, _u64, _u8p, _vp, _u8p, _u8p, _vp, _u32]),
+    "hbg_sig_verify_shares": (_i, [_vp, _u32, _u8p, _vp, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_test_bls": (_i, [_vp, C.c_int, _u32, _vp, _u32, _vp, _u32]),
     "hbg_test_set_tdec_batched": (_i, [_vp, C.c_int]),
 }

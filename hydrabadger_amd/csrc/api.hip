@@ -44,6 +44,7 @@ struct hbg_ctx {
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> enc_plans; // device shared encode plans
     // share verification schedule (hbg_test_set_tdec_batched / HBG_TDEC_BATCHED): 0 per share, 1 batched
     // (pk fixed-base tables when each key verifies >= kPkTableMinUses shares), 2 batched + tables always
+    // (and, for signature shares, no speculative 16-group round)
     int tdec_batched = 1;
     std::mutex mu;
 };
@@ -921,6 +922,148 @@ int hbg_sig_combine(hbg_ctx* c, uint32_t t, uint64_t n, const uint8_t* share96, 
     HBG_TRY(bls::launch_coin_combine((uint32_t)n, t, (const uint8_t*)dsh, (const uint32_t*)dix, (uint8_t*)dsig,
                                      (uint8_t*)dpar, (int32_t*)dst, c->stream));
     return drain(c, flags, {{sig96, {dsig, 96ull * n}}, {parity, {dpar, n}}, {status, {dst, 4ull * n}}});
+}
+
+namespace {
+constexpr uint32_t kSigCheckChunk = 131072;  // check items / shares per launch (G2Prepared scratch: 19.6 KB each)
+constexpr uint64_t kSigSpecItems = 131072;   // 2 waves per SIMD of 256 CUs x 4 SIMDs x 64 lanes
+
+// One check round over n_items items (device list `items`, or every batch
+// when null), chunked so the per-lane G2Prepared scratch stays bounded.
+int sig_check_round(hbg_ctx* c, uint32_t n_items, uint32_t spec, const bls::CheckItem* items,
+                    const bls::BatchDesc* desc,
+                    const uint32_t* perm, const uint32_t* sums, const uint8_t* lok, const uint32_t* coefH,
+                    uint8_t* dok, bls::CheckItem* next, uint32_t* next_n, uint32_t* fails, uint32_t* fail_n) {
+    if (n_items == 0) return HBG_OK;
+    const uint32_t chunk = n_items < kSigCheckChunk ? n_items : kSigCheckChunk;
+    void* lines;
+    HBG_CHECK(scratch(c, 14, 4ull * bls::kLineWordsPerPoint * chunk, &lines));
+    for (uint32_t i0 = 0; i0 < n_items; i0 += chunk) {
+        const uint32_t m = (n_items - i0) < chunk ? (n_items - i0) : chunk;
+        HBG_TRY(bls::launch_sig_batch_check(m, i0, spec, items, desc, perm, sums, lok, coefH, (uint32_t*)lines, dok, next,
+                                            next_n, fails, fail_n, c->stream));
+    }
+    return HBG_OK;
+}
+
+int sig_verify_sel(hbg_ctx* c, uint64_t n, const uint32_t* sel, const uint8_t* dsh, const uint32_t* dsd,
+                   const uint32_t* dsp, const uint32_t* paff, const int32_t* pst, const uint32_t* coefH,
+                   uint8_t* dok) {
+    if (n == 0) return HBG_OK;
+    const uint64_t chunk = n < kSigCheckChunk ? n : kSigCheckChunk;
+    void* lines;
+    HBG_CHECK(scratch(c, 14, 4ull * bls::kLineWordsPerPoint * chunk, &lines));
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+        const uint64_t m = (n - k0) < chunk ? (n - k0) : chunk;
+        HBG_TRY(bls::launch_sig_verify_shares(m, k0, sel, dsh, dsd, dsp, paff, pst, coefH, (uint32_t*)lines, dok,
+                                              c->stream));
+    }
+    return HBG_OK;
+}
+}  // namespace
+
+int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const uint64_t* doc_off, uint32_t n_pk,
+                          const uint8_t* pk48, uint64_t n, const uint8_t* share96, const uint32_t* share_doc,
+                          const uint32_t* share_pk, uint8_t* ok, uint32_t flags) {
+    if (!c || (n && (!doc_off || !pk48 || !share96 || !share_doc || !share_pk || !ok || n_pk == 0 || n_doc == 0)))
+        return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!index_ok(flags, share_doc, n, n_doc) || !index_ok(flags, share_pk, n, n_pk)) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t dlen = (flags & HBG_DEVICE) ? 0 : doc_off[n_doc];
+    const void *dpk, *dd, *doff, *dsh, *dsd, *dsp;
+    void *dok, *paff, *pst, *coefH, *seeds;
+    HBG_CHECK(stage_in(c, flags, 0, pk48, 48ull * n_pk, &dpk));
+    HBG_CHECK(stage_in(c, flags, 1, share_doc, 4ull * n, &dsd));
+    HBG_CHECK(stage_in(c, flags, 2, doc, dlen, &dd));
+    HBG_CHECK(stage_in(c, flags, 3, doc_off, 8ull * (n_doc + 1), &doff));
+    HBG_CHECK(stage_in(c, flags, 9, share96, 96ull * n, &dsh));
+    HBG_CHECK(stage_in(c, flags, 10, share_pk, 4ull * n, &dsp));
+    HBG_CHECK(stage_out(c, flags, 4, ok, n, &dok));
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
+    HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
+    HBG_CHECK(scratch(c, 7, 4ull * bls::kLineWordsPerPoint * n_doc, &coefH));
+    HBG_CHECK(scratch(c, 8, 32ull * n_doc, &seeds));
+    HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    HBG_TRY(bls::launch_sig_doc_prepare(n_doc, (const uint8_t*)dd, (const uint64_t*)doff, (uint32_t*)coefH,
+                                        (uint8_t*)seeds, c->stream));
+    const uint32_t *sd = (const uint32_t*)dsd, *sp = (const uint32_t*)dsp, *pa = (const uint32_t*)paff;
+    const int32_t* ps = (const int32_t*)pst;
+    const uint8_t* sh = (const uint8_t*)dsh;
+    uint8_t* o = (uint8_t*)dok;
+    if (!(c->tdec_batched && n >= 2 && n < (1ull << 31))) {
+        HBG_CHECK(sig_verify_sel(c, n, nullptr, sh, sd, sp, pa, ps, (const uint32_t*)coefH, o));
+        return drain(c, flags, {{ok, {dok, n}}});
+    }
+    // batched: sort by document, batches of <= 64, weighted sums, 4-ary group testing
+    const uint32_t nn = (uint32_t)n;
+    uint32_t* tbl = nullptr;
+    if (c->tdec_batched == 2 || n >= kPkTableMinUses * n_pk) {
+        void* p;
+        HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
+        tbl = (uint32_t*)p;
+        HBG_TRY(bls::launch_tdec_pk_table(n_pk, pa, tbl, c->stream));
+    }
+    void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
+    const size_t tb_bytes = bls::tdec_batch_temp_bytes(nn);
+    HBG_CHECK(scratch(c, 16, 4ull * n, &keys));
+    HBG_CHECK(scratch(c, 17, 4ull * n, &perm));
+    HBG_CHECK(scratch(c, 18, 4ull * n, &ta));
+    HBG_CHECK(scratch(c, 19, 4ull * n, &tb));
+    HBG_CHECK(scratch(c, 20, (size_t)bls::kBatchDescBytes * n, &desc));
+    HBG_CHECK(scratch(c, 21, tb_bytes, &temp));
+    HBG_CHECK(scratch(c, 22, 64, &cnt));
+    uint32_t nbh[2] = {0, 0};
+    HBG_TRY(bls::launch_tdec_batch_plan(nn, n_doc, sd, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta,
+                                        (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, nbh, c->stream));
+    const uint32_t nb = nbh[0] + nbh[1];
+    void *sums, *lok, *items, *items2, *fails;
+    HBG_CHECK(scratch(c, 23, (size_t)bls::kSigBatchSumBytes * nb, &sums));
+    HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
+    HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 4 * nb, &items));
+    HBG_CHECK(scratch(c, 28, (size_t)bls::kCheckItemBytes * 16 * nb, &items2));
+    HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
+    uint32_t* counts = (uint32_t*)cnt;  // [0] 16-group items, [1] failing shares, [2] quad items
+    const bls::BatchDesc* ds = (const bls::BatchDesc*)desc;
+    const uint32_t *pm = (const uint32_t*)perm, *sm = (const uint32_t*)sums, *ch = (const uint32_t*)coefH;
+    const uint8_t* lk = (const uint8_t*)lok;
+    HBG_TRY(hipMemsetAsync(o, 0, n, c->stream));
+    HBG_TRY(hipMemsetAsync(counts, 0, 16, c->stream));
+    HBG_TRY(bls::launch_sig_batch_leaves(nb, ds, pm, sh, sp, (const uint8_t*)seeds, pa, ps, tbl, (uint32_t*)sums,
+                                         (uint8_t*)lok, c->stream));
+    uint32_t h[3];
+    // Check rounds run one pairing per lane and are latency-bound below ~1 wave
+    // per SIMD; while 5 items per batch still fit one such wave per SIMD, the
+    // 16-groups are checked speculatively in round 0 (one round fewer).
+    // (test mode 2 always takes the plain rounds so both schedules stay covered)
+    const bool spec = c->tdec_batched != 2 && (uint64_t)nb * 5u <= kSigSpecItems;
+    if (spec) {
+        HBG_CHECK(sig_check_round(c, nb * 5u, 1, nullptr, ds, pm, sm, lk, ch, o, (bls::CheckItem*)items2, counts + 2,
+                                  (uint32_t*)fails, counts + 1));
+    } else {
+        // round 0: every batch; failing batches push their 16-share groups
+        HBG_CHECK(sig_check_round(c, nb, 0, nullptr, ds, pm, sm, lk, ch, o, (bls::CheckItem*)items, counts,
+                                  (uint32_t*)fails, counts + 1));
+        HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
+        HBG_TRY(hipStreamSynchronize(c->stream));
+        // round 1: 16-share groups; failing ones push their quads
+        HBG_CHECK(sig_check_round(c, h[0], 0, (const bls::CheckItem*)items, ds, pm, sm, lk, ch, o,
+                                  (bls::CheckItem*)items2, counts + 2, (uint32_t*)fails, counts + 1));
+    }
+    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    // round 2: quads; failing ones append their shares
+    HBG_CHECK(sig_check_round(c, h[2], 0, (const bls::CheckItem*)items2, ds, pm, sm, lk, ch, o, nullptr, nullptr,
+                              (uint32_t*)fails, counts + 1));
+    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    if (getenv("HBG_TDEC_DEBUG"))
+        fprintf(stderr, "hbg batched sig verify: n=%u batches=%u 16-groups=%u quads=%u fail-shares=%u\n", nn, nb,
+                h[0], h[2], h[1]);
+    // round 3: the shares of failing quads, one by one (the reference's equation)
+    HBG_CHECK(sig_verify_sel(c, h[1], (const uint32_t*)fails, sh, sd, sp, pa, ps, ch, o));
+    return drain(c, flags, {{ok, {dok, n}}});
 }
 
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {

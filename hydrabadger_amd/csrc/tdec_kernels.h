@@ -15,6 +15,7 @@ constexpr uint32_t kBatchShares = 64;             // batched verification: share
 struct BatchDesc;
 struct CheckItem;
 constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 21 * 2 * 36 * 4;
+constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G2 Jacobian sums of 21 tree nodes
 
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
@@ -53,6 +54,21 @@ hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const in
                                      int32_t* status, hipStream_t st);
 hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, const uint32_t* idx, uint8_t* sig96,
                                uint8_t* parity, int32_t* status, hipStream_t st);
+hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t* off, uint32_t* coefH,
+                                  uint8_t* seeds, hipStream_t st);
+hipError_t launch_sig_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share96,
+                                   const uint32_t* share_pk, const uint8_t* seeds, const uint32_t* pk_aff,
+                                   const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
+                                   uint8_t* leaf_ok, hipStream_t st);
+hipError_t launch_sig_batch_check(uint32_t n_items, uint32_t base, uint32_t spec, const CheckItem* items,
+                                  const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
+                                  const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
+                                  CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
+                                  hipStream_t st);
+hipError_t launch_sig_verify_shares(uint64_t n, uint64_t base, const uint32_t* sel, const uint8_t* share96,
+                                    const uint32_t* share_doc, const uint32_t* share_pk, const uint32_t* pk_aff,
+                                    const int32_t* pk_status, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
+                                    hipStream_t st);
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,

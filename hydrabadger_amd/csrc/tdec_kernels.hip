@@ -633,6 +633,45 @@ TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
     }
 }
 
+// Node geometry of a check item in its batch's 4-ary tree: leaf lanes [l0, l1).
+BD uint32_t node_size(uint32_t node) { return node == kNodeBatch ? 64u : (node >= kNode16 ? 16u : 4u); }
+BD uint32_t node_first(uint32_t node) {
+    return node == kNodeBatch ? 0u : (node >= kNode16 ? 16u * (node - kNode16) : 4u * node);
+}
+BD bool node_any_valid(const uint8_t* lok, uint32_t l0, uint32_t l1) {
+    bool any = false;
+    for (uint32_t l = l0; l < l1; ++l) any |= lok[l] != 0;
+    return any;
+}
+
+// One group-testing step for a checked node: a pass vouches for the node's
+// valid leaves; a failing batch / 16-group pushes its (non-empty) four
+// children; a failing quad appends its valid leaves to the per-share list.
+// With `children_checked` (a speculative round that checked a batch together
+// with its four 16-groups) a failing batch pushes nothing.
+BD void batch_tree_step(bool pass, const CheckItem& it, const BatchDesc& d, const uint8_t* lok,
+                        const uint32_t* __restrict__ perm, uint8_t* __restrict__ ok, CheckItem* __restrict__ next,
+                        uint32_t* __restrict__ next_n, uint32_t* __restrict__ fail_list,
+                        uint32_t* __restrict__ fail_n, bool children_checked = false) {
+    const uint32_t size = node_size(it.node), l0 = node_first(it.node), l1 = l0 + size;
+    if (pass) {
+        for (uint32_t l = l0; l < l1; ++l)
+            if (lok[l]) ok[perm[d.start + l]] = 1;
+    } else if (children_checked) {
+        return;
+    } else if (size > 4u) {  // four children of a quarter the size
+        const uint32_t cs = size / 4u;
+        for (uint32_t c = 0; c < 4; ++c) {
+            const uint32_t c0 = l0 + c * cs;
+            const uint32_t node = size == 64u ? kNode16 + c : c0 / 4u;
+            if (node_any_valid(lok, c0, c0 + cs)) next[atomicAdd(next_n, 1u)] = CheckItem{it.b, node};
+        }
+    } else {
+        for (uint32_t l = l0; l < l1; ++l)
+            if (lok[l]) fail_list[atomicAdd(fail_n, 1u)] = perm[d.start + l];
+    }
+}
+
 // One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.
 TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict__ items,
                                                        const BatchDesc* __restrict__ desc,
@@ -649,35 +688,16 @@ TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict_
     if (i >= n_items) return;
     const CheckItem it = items ? items[i] : CheckItem{i, kNodeBatch};
     const BatchDesc d = desc[it.b];
-    const uint32_t size = it.node == kNodeBatch ? 64u : (it.node >= kNode16 ? 16u : 4u);
-    const uint32_t l0 = it.node == kNodeBatch ? 0u : (it.node >= kNode16 ? 16u * (it.node - kNode16) : 4u * it.node);
-    const uint32_t l1 = l0 + size;
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
-    bool any = false;
-    for (uint32_t l = l0; l < l1; ++l) any |= lok[l] != 0;
-    if (!any) return;  // nothing valid to vouch for: those shares stay 0
+    const uint32_t l0 = node_first(it.node);
+    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;  // nothing valid to vouch for: those shares stay 0
     const uint32_t* sm = sums + (uint64_t)it.b * kBatchSumWords + it.node * kSumWords;
     const G1A a = g1_to_affine(load_jac(sm)), bb = g1_to_affine(load_jac(sm + kJacWords));
     const bool w_inf = ct_u[32ull * d.ct + 25] != 0;
     const bool pass = pairing_check2(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, !a.inf,
                                      coefW + (uint64_t)d.ct * kLineWordsPerPoint, bb.x, fp_neg(bb.y),
                                      !bb.inf && !w_inf);
-    if (pass) {
-        for (uint32_t l = l0; l < l1; ++l)
-            if (lok[l]) ok[perm[d.start + l]] = 1;
-    } else if (size > 4u) {  // four children of a quarter the size
-        const uint32_t cs = size / 4u;
-        for (uint32_t c = 0; c < 4; ++c) {
-            const uint32_t c0 = l0 + c * cs;
-            bool v = false;
-            for (uint32_t l = c0; l < c0 + cs; ++l) v |= lok[l] != 0;
-            const uint32_t node = size == 64u ? kNode16 + c : c0 / 4u;
-            if (v) next[atomicAdd(next_n, 1u)] = CheckItem{it.b, node};
-        }
-    } else {
-        for (uint32_t l = l0; l < l1; ++l)
-            if (lok[l]) fail_list[atomicAdd(fail_n, 1u)] = perm[d.start + l];
-    }
+    batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n);
 }
 
 TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
@@ -1140,6 +1160,183 @@ TDEC_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
     parity[g] = (uint8_t)(__builtin_popcount(x) & 1u);
 }
 
+// ---------------------------------------------------------------- batched signature-share verification
+// PublicKeyShare::verify(sig_i, doc) (threshold_sign / common coin, SURVEY.md
+// §8(f3)) for the shares of ONE document: e(pk_i, H) == e(G1, sig_i) for all
+// i  <=  e(sum r_i pk_i, H) == e(G1, sum r_i sig_i), H = hash_g2(doc) hashed
+// and prepared ONCE per document (the per-share bls_verify hashes to G2 and
+// prepares H once per share).  Same Fiat-Shamir weights, 4-ary group-testing
+// tree and per-share fallback as the decryption shares above, so every 0 bit
+// is the reference's per-share equation and a 1 from a passing (sub)batch is
+// wrong with probability <= 2^-63.
+constexpr uint32_t kG2JacWords = 72;
+constexpr uint32_t kSigSumWords = kJacWords + kG2JacWords;  // (sum r pk: G1, sum r sig: G2)
+constexpr uint32_t kSigBatchSumWords = kNodes * kSigSumWords;
+
+BD void store_g2jac(uint32_t* d, const G2& p) {
+    store_fp(d, p.x.c0);
+    store_fp(d + 12, p.x.c1);
+    store_fp(d + 24, p.y.c0);
+    store_fp(d + 36, p.y.c1);
+    store_fp(d + 48, p.z.c0);
+    store_fp(d + 60, p.z.c1);
+}
+BD G2 load_g2jac(const uint32_t* d) {
+    return {{load_fp(d), load_fp(d + 12)}, {load_fp(d + 24), load_fp(d + 36)}, {load_fp(d + 48), load_fp(d + 60)}};
+}
+
+// per document: seed = SHA3-256(doc) (the ChaCha seed of hash_g2), G2Prepared lines of H
+TDEC_KERNEL void sig_doc_prepare(uint32_t n, const uint8_t* __restrict__ doc, const uint64_t* __restrict__ off,
+                                 uint32_t* __restrict__ coefH, uint8_t* __restrict__ seeds) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint8_t seed[32];
+    sha3_bytes(doc + off[k], (uint32_t)(off[k + 1] - off[k]), seed);
+    for (int i = 0; i < 32; ++i) seeds[32ull * k + i] = seed[i];
+    const G2A h = hash_g2_from_seed(seed);
+    g2_prepare(h.x, h.y, coefH + (uint64_t)k * kLineWordsPerPoint);
+}
+
+// One 64-lane block per batch (shares of one document), lane = share: decode
+// the G2 share with the crate's subgroup check, weight r_i = SHA3(D || i)
+// (D = SHA3 of the leaf digests SHA3(doc seed || share || key index)), then
+// [r_i] sig_i (G2) and [r_i] pk_i (G1, fixed-base tables when given) and the
+// quad / 16-group / batch sums by cross-lane butterflies.
+TDEC_KERNEL void sig_batch_leaves(const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
+                                  const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_pk,
+                                  const uint8_t* __restrict__ seeds, const uint32_t* __restrict__ pk_aff,
+                                  const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ pk_tbl,
+                                  uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
+    __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    const BatchDesc d = desc[b];
+    const uint32_t q = d.start + lane;
+    const bool in = q < d.end;
+    const uint32_t k = in ? perm[q] : 0u;
+    const uint32_t pk = in ? share_pk[k] : 0u;
+    bool valid = in && pk_status[pk] == 0;
+    G2A s;
+    if (valid) valid = g2_decompress(share96 + 96ull * k, s, true);
+    if (in) {
+        uint8_t m[32 + 96 + 4];
+        for (int i = 0; i < 32; ++i) m[i] = seeds[32ull * d.ct + i];
+        for (int i = 0; i < 96; ++i) m[32 + i] = share96[96ull * k + i];
+        for (int i = 0; i < 4; ++i) m[128 + i] = (uint8_t)(pk >> (8 * i));
+        sha3_bytes(m, sizeof(m), sDig + 32 * lane);
+    }
+    __syncthreads();
+    if (lane == 0) sha3_bytes(sDig, 32u * (d.end - d.start), sBatch);
+    __syncthreads();
+    uint64_t r = 0;
+    if (valid) {
+        uint8_t m[36], dg[32];
+        for (int i = 0; i < 32; ++i) m[i] = sBatch[i];
+        for (int i = 0; i < 4; ++i) m[32 + i] = (uint8_t)(lane >> (8 * i));
+        sha3_bytes(m, 36, dg);
+        for (int i = 0; i < 8; ++i) r |= (uint64_t)dg[i] << (8 * i);
+        r |= 1ull;  // nonzero
+    }
+    leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
+    uint32_t* out = sums + (uint64_t)b * kSigBatchSumWords;
+    // G1 side: sum r_i pk_i
+    {
+        G1 B = {fp_one(), fp_one(), fp_zero()};
+        const uint32_t* pa = pk_aff + 32ull * pk;
+        if (valid && pa[24] == 0) {
+            if (pk_tbl) {
+                const uint32_t* t = pk_tbl + (uint64_t)pk * kPkTblWords;
+                for (int w = 0; w < 8; ++w) {
+                    const uint32_t v = (uint32_t)(r >> (8 * w)) & 255u;
+                    if (v) {
+                        const uint32_t* e = t + (w * 256 + v) * 24;
+                        B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+                    }
+                }
+            } else {
+                B = g1_mul_u64(load_fp(pa), load_fp(pa + 12), r);
+            }
+        }
+#pragma unroll 1
+        for (int m = 1; m < 64; m <<= 1) {
+            B = g1_add(B, g1_shfl_xor(B, m));
+            if (m == 2 && (lane & 3u) == 0) store_jac(out + (lane >> 2) * kSigSumWords, B);
+            if (m == 8 && (lane & 15u) == 0) store_jac(out + (kNode16 + (lane >> 4)) * kSigSumWords, B);
+        }
+        if (lane == 0) store_jac(out + kNodeBatch * kSigSumWords, B);
+    }
+    // G2 side: sum r_i sig_i
+    {
+        G2 A = {fp2_one(), fp2_one(), fp2_zero()};
+        if (valid && !s.inf) A = g2_mul_u64(s.x, s.y, r);
+#pragma unroll 1
+        for (int m = 1; m < 64; m <<= 1) {
+            A = g2_add(A, g2_shfl_xor(A, m));
+            if (m == 2 && (lane & 3u) == 0) store_g2jac(out + (lane >> 2) * kSigSumWords + kJacWords, A);
+            if (m == 8 && (lane & 15u) == 0)
+                store_g2jac(out + (kNode16 + (lane >> 4)) * kSigSumWords + kJacWords, A);
+        }
+        if (lane == 0) store_g2jac(out + kNodeBatch * kSigSumWords + kJacWords, A);
+    }
+}
+
+// e(pk, H) * e(-G1, sig) == 1 with H's lines prepared; sig's lines go to `ls`.
+BD bool sig_pair_check(const uint32_t* coefH, const Fp& pkx, const Fp& pky, bool pk_inf, const G2A& sig,
+                       uint32_t* ls) {
+    if (!sig.inf) g2_prepare(sig.x, sig.y, ls);
+    return pairing_check2(coefH, pkx, pky, !pk_inf, ls, fp_const(kG1x), fp_neg(fp_const(kG1y)), !sig.inf);
+}
+
+// One lane per check item (item base + i; items == null: round 0 over every
+// batch, or with `spec` over every batch AND its four 16-groups, item
+// 5b + j, so a small batch count does not pay a separate latency-bound round
+// for the 16-groups); lines: one G2Prepared slot per lane of this launch.
+TDEC_KERNEL void sig_batch_check(uint32_t n_items, uint32_t base, uint32_t spec, const CheckItem* __restrict__ items,
+                                 const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
+                                 const uint32_t* __restrict__ sums, const uint8_t* __restrict__ leaf_ok,
+                                 const uint32_t* __restrict__ coefH, uint32_t* __restrict__ lines,
+                                 uint8_t* __restrict__ ok, CheckItem* __restrict__ next,
+                                 uint32_t* __restrict__ next_n, uint32_t* __restrict__ fail_list,
+                                 uint32_t* __restrict__ fail_n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_items) return;
+    const uint32_t j = base + i;
+    const CheckItem it = items ? items[j]
+                               : (spec ? CheckItem{j / 5u, j % 5u == 0 ? kNodeBatch : kNode16 + j % 5u - 1u}
+                                       : CheckItem{j, kNodeBatch});
+    const BatchDesc d = desc[it.b];
+    const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
+    const uint32_t l0 = node_first(it.node);
+    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;
+    const uint32_t* sm = sums + (uint64_t)it.b * kSigBatchSumWords + it.node * kSigSumWords;
+    const G1A a = g1_to_affine(load_jac(sm));
+    const G2A sg = g2_to_affine(load_g2jac(sm + kJacWords));
+    const bool pass = sig_pair_check(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, a.inf, sg,
+                                     lines + (uint64_t)i * kLineWordsPerPoint);
+    batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n,
+                    spec && !items && it.node == kNodeBatch);
+}
+
+// Per-share PublicKeyShare::verify with H prepared per document: share
+// sel[base + i] (or base + i), lines: one G2Prepared slot per lane.
+TDEC_KERNEL void sig_verify_shares(uint64_t n, uint64_t base, const uint32_t* __restrict__ sel,
+                                   const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_doc,
+                                   const uint32_t* __restrict__ share_pk, const uint32_t* __restrict__ pk_aff,
+                                   const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ coefH,
+                                   uint32_t* __restrict__ lines, uint8_t* __restrict__ ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = sel ? sel[base + i] : base + i;
+    const uint32_t p = share_pk[k];
+    G2A sig;
+    bool good = pk_status[p] == 0 && g2_decompress(share96 + 96ull * k, sig, true);
+    if (good) {
+        const uint32_t* pa = pk_aff + 32ull * p;
+        good = sig_pair_check(coefH + (uint64_t)share_doc[k] * kLineWordsPerPoint, load_fp(pa), load_fp(pa + 12),
+                              pa[24] != 0, sig, lines + i * kLineWordsPerPoint);
+    }
+    ok[k] = good ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ unit-test hook
 // op: 0 fp_mul(a,b)  1 fp_inv(a)  2 fp2_sqrt(a)  3 g1_decompress  4 g2_decompress
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
@@ -1370,5 +1567,44 @@ hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* ou
 }
 
 #undef BD
+
+hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t* off, uint32_t* coefH,
+                                  uint8_t* seeds, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    sig_doc_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, doc, off, coefH, seeds);
+    return hipGetLastError();
+}
+hipError_t launch_sig_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share96,
+                                   const uint32_t* share_pk, const uint8_t* seeds, const uint32_t* pk_aff,
+                                   const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
+                                   uint8_t* leaf_ok, hipStream_t st) {
+    if (nb == 0) return hipSuccess;
+    sig_batch_leaves<<<dim3(nb), dim3(64), 0, st>>>(desc, perm, share96, share_pk, seeds, pk_aff, pk_status, pk_tbl,
+                                                    sums, leaf_ok);
+    return hipGetLastError();
+}
+hipError_t launch_sig_batch_check(uint32_t n_items, uint32_t base, uint32_t spec, const CheckItem* items,
+                                  const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
+                                  const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
+                                  CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
+                                  hipStream_t st) {
+    if (n_items == 0) return hipSuccess;
+    sig_batch_check<<<dim3((n_items + 63) / 64), dim3(64), 0, st>>>(n_items, base, spec, items, desc, perm, sums,
+                                                                    leaf_ok,
+                                                                    coefH, lines, ok, next, next_n, fail_list,
+                                                                    fail_n);
+    return hipGetLastError();
+}
+hipError_t launch_sig_verify_shares(uint64_t n, uint64_t base, const uint32_t* sel, const uint8_t* share96,
+                                    const uint32_t* share_doc, const uint32_t* share_pk, const uint32_t* pk_aff,
+                                    const int32_t* pk_status, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
+                                    hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    sig_verify_shares<<<dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st>>>(n, base, sel, share96, share_doc,
+                                                                            share_pk, pk_aff, pk_status, coefH,
+                                                                            lines, ok);
+    return hipGetLastError();
+}
+
 }  // namespace bls
 }  // namespace hbg

@@ -11,6 +11,7 @@ as hbbft's ``ThresholdDecrypt`` uses it, reached from
   SecretKey.decrypt_share_no_verify(ct)                -> hbg_tdec_decrypt_shares (§8 f1)
   SecretKey.sign(msg) / PublicKey.verify(sig, msg)     -> hbg_bls_sign / hbg_bls_verify (§8 f2,
                                                           src/lib.rs:405-416, :434)
+  PublicKeyShare.verify(sig_share, doc) (coin shares)  -> hbg_sig_verify_shares  (§8 f3 coin)
   combine_signatures(t, shares) (+ Signature::parity)  -> hbg_sig_combine        (§8 f3 coin)
 
 Points are the crate's zcash-compressed bytes (G1 48 B, G2 96 B).  Every
@@ -246,6 +247,24 @@ class PublicKey:
 
 
 # --------------------------------------------------------------------------- SURVEY.md §8(f3)
+def verify_sig_shares_batch(pk48s: list, docs: list, items: list, ctx=None) -> np.ndarray:
+    """PublicKeyShare::verify(sig_share, doc) for many signature shares:
+    items = [(doc index, pk index, sig96)] -> ok bits (identical to
+    verify_sig_batch on the same triples; hash_g2 once per document)."""
+    n = len(items)
+    if n == 0:
+        return np.zeros(0, np.uint8)
+    buf, off = _msg_table(docs)
+    pk = np.frombuffer(b"".join(bytes(p) for p in pk48s), np.uint8).copy()
+    sd = np.array([d for d, _, _ in items], np.uint32)
+    sp = np.array([p for _, p, _ in items], np.uint32)
+    sig = np.frombuffer(b"".join(bytes(s) for _, _, s in items), np.uint8).copy()
+    ok = np.zeros(n, np.uint8)
+    check(lib().hbg_sig_verify_shares((ctx or default_context()).h, len(docs), ptr(buf), ptr(off), len(pk48s), ptr(pk),
+                                      n, ptr(sig), ptr(sd), ptr(sp), ptr(ok), 0), "PublicKeyShare::verify")
+    return ok
+
+
 def sig_combine_batch(t: int, shares: list, ctx=None):
     """PublicKeySet::combine_signatures + Signature::parity for many coins:
     shares[k] = the first t+1 (node index, 96-B signature share) items.

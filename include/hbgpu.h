@@ -224,6 +224,21 @@ int hbg_sig_combine(hbg_ctx *ctx, uint32_t t, uint64_t n, const uint8_t *share96
                     const uint32_t *share_index, uint8_t *sig96, uint8_t *parity,
                     int32_t *status, uint32_t flags);
 
+/* PublicKeyShare::verify(share, doc) for n signature shares grouped by
+ * document (the coin nonce every node signs): share k (share96[k]) claims to
+ * sign doc share_doc[k] (doc[doc_off[d] .. doc_off[d+1]]) under public key
+ * share pk48[share_pk[k]].  ok[k] is bit-identical to hbg_bls_verify on the
+ * same (pk, doc, share): 1 iff the key and the share decode (subgroup checks)
+ * and e(pk, hash_g2(doc)) == e(G1, share).  hash_g2 runs once per document
+ * and shares of one document are checked in weighted batches (a failing
+ * batch falls back to the per-share equation); HBG_TDEC_BATCHED=0 /
+ * hbg_test_set_tdec_batched(ctx, 0) select the per-share schedule.  Replaces
+ * hbbft ThresholdSign::handle_message's PublicKeyShare::verify (reached from
+ * src/hydrabadger/state.rs:487). */
+int hbg_sig_verify_shares(hbg_ctx *ctx, uint32_t n_doc, const uint8_t *doc, const uint64_t *doc_off,
+                          uint32_t n_pk, const uint8_t *pk48, uint64_t n, const uint8_t *share96,
+                          const uint32_t *share_doc, const uint32_t *share_pk, uint8_t *ok, uint32_t flags);
+
 /* Device-side seeded generator: row k of out gets nbytes of
  * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */
 int hbg_synth_bytes(hbg_ctx *ctx, uint32_t tag, uint64_t first_instance, uint64_t nbytes,

@@ -175,3 +175,59 @@ def test_coin_combine_arbitrary_points(t):
             assert st[k] == _lib.HBG_E_INVALID_POINT
         else:
             assert st[k] == 0 and sigs[k] == e[0] and bool(par[k]) == e[1], k
+
+
+@pytest.mark.parametrize("seed,bad_rate", [(1, 0.0), (2, 0.03), (3, 0.4)])
+def test_coin_share_verify_batched(seed, bad_rate):
+    """§8(f3) hbg_sig_verify_shares (PublicKeyShare::verify of coin shares,
+    hash_g2 once per document, weighted batches + group testing) gives the
+    same bits as the per-share hbg_bls_verify and as the expected validity, in
+    every schedule (batched, batched + fixed-base key tables, per share):
+    batches crossing 64, ragged documents, wrong-key claims, shares of another
+    document, undecodable / tampered / identity shares, an undecodable key."""
+    th = _th()
+    from hydrabadger_amd import _lib
+    s = scenario()
+    ks, n = s["ks"], len(s["pk_shares"])
+    sks = [ks.secret_key_share(i) for i in range(n)]
+    pks = [B.g1_compress(p) for p in s["pk_shares"]]
+    junk_pk = bytearray(pks[0]); junk_pk[0] &= 0x7F
+    pks.append(bytes(junk_pk))                                   # key index n: undecodable
+    rng = random.Random(seed)
+    docs = [bytes(rng.randrange(256) for _ in range(L)) for L in (0, 17, 64, 200, 9)]
+    signed = th.sign_batch(sks, [(i, d) for d in docs for i in range(n)])
+    good = {(d, i): signed[d * n + i] for d in range(len(docs)) for i in range(n)}
+    items, expect = [], []
+    for d, count in enumerate((150, 64, 5, 65, 1)):
+        for q in range(count):
+            i = rng.randrange(n)
+            r = rng.random()
+            if r < bad_rate / 3:
+                items.append((d, (i + 1) % n, good[(d, i)])); expect.append(0)          # wrong key
+            elif r < 2 * bad_rate / 3:
+                items.append((d, i, good[((d + 1) % len(docs), i)])); expect.append(0)  # another doc's share
+            elif r < bad_rate:
+                t = bytearray(good[(d, i)]); t[40] ^= 1                                 # tampered x
+                items.append((d, i, bytes(t))); expect.append(0)
+            else:
+                items.append((d, i, good[(d, i)])); expect.append(1)
+    junk = bytearray(good[(0, 1)]); junk[0] &= 0x7F
+    inf = bytearray(96); inf[0] = 0xC0
+    items += [(0, 1, bytes(junk)), (3, 2, bytes(inf)), (1, n, good[(1, 0)])]
+    expect += [0, 0, 0]
+    order = list(range(len(items)))
+    rng.shuffle(order)
+    items = [items[k] for k in order]
+    expect = np.array([expect[k] for k in order], np.uint8)
+    ref = th.verify_sig_batch(pks, [(p, docs[d], sg) for d, p, sg in items])
+    assert np.array_equal(ref, expect)
+    ctx = _lib.Context(0)
+    try:
+        outs = []
+        for mode in (1, 2, 0):
+            _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
+            outs.append(th.verify_sig_shares_batch(pks, docs, items, ctx))
+    finally:
+        ctx.close()
+    for o in outs:
+        assert np.array_equal(o, expect)
