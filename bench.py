@@ -76,6 +76,8 @@ def parse():
                     help="SURVEY.md §8(f1): ciphertexts encrypted + x64 decryption shares (0 disables)")
     ap.add_argument("--coins", type=int, default=16384,
                     help="SURVEY.md §8(f3): common coins (x64 signature shares) signed, verified, combined (0 disables)")
+    ap.add_argument("--wire-instances", type=int, default=1024,
+                    help="SURVEY.md §8(f4): instances whose N Value messages are written/parsed/validated (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     return ap.parse_args()
@@ -388,6 +390,61 @@ def coin_leg(ctx, dev, n_coins: int, n_nodes: int, reps: int):
             "heads_fraction": float(par.float().mean().item()), "all_ok": good}
 
 
+def broadcast_wire_leg(ctx, dev, shards, levels, L: int, n_inst: int, reps: int):
+    """SURVEY.md §8(f4): every Value message (bincode Message::Value(proof(i)))
+    of n_inst encoded N=64 instances written from the shard batch + levels,
+    parsed back into the validate table, and validated (Proof::validate)."""
+    from hydrabadger_amd import _lib
+    from hydrabadger_amd import broadcast as bc
+    N = shards.shape[1]
+    S = shards.shape[2]
+    m = n_inst * N
+    idx = np.tile(np.arange(N, dtype=np.uint32), n_inst)
+    off = bc.proof_msg_offsets(N, L, idx)
+    total = int(off[-1])
+    d_inst = torch.from_numpy(np.repeat(np.arange(n_inst, dtype=np.int64), N)).to(dev)
+    d_idx = torch.from_numpy(idx.astype(np.int32)).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    depth = _lib.merkle_depth(N)
+    tag = torch.empty(m, dtype=torch.int32, device=dev)
+    vals = torch.empty((m, S), dtype=torch.uint8, device=dev)
+    rindex = torch.empty(m, dtype=torch.int32, device=dev)
+    dig = torch.empty((m, depth, 32), dtype=torch.uint8, device=dev)
+    nd = torch.empty(m, dtype=torch.int32, device=dev)
+    roots = torch.empty((m, 32), dtype=torch.uint8, device=dev)
+    st = torch.empty(m, dtype=torch.int32, device=dev)
+    ok = torch.empty(m, dtype=torch.uint8, device=dev)
+    A = _lib.HBG_DEVICE | _lib.HBG_ASYNC
+
+    def write():
+        bc.write_proof_msgs_batch(N, L, shards, levels, bc.Message.VALUE, d_inst, d_idx, out, d_off, ctx=ctx,
+                                  device=True, asynchronous=True)
+
+    def read():
+        bc.read_msgs_batch(N, L, out, d_off, tag, vals, rindex, dig, nd, roots, st, ctx=ctx, device=True,
+                           asynchronous=True)
+
+    def validate():
+        _lib.check(_lib.lib().hbg_merkle_validate(ctx.h, N, L, _lib.ptr(vals), S, _lib.ptr(rindex), _lib.ptr(dig),
+                                                  _lib.ptr(nd), _lib.ptr(roots), _lib.ptr(ok), m, A), "validate")
+    write()
+    read()
+    validate()
+    torch.cuda.synchronize()
+    good = (bool((st == 0).all().item()) and bool((ok == 1).all().item())
+            and bool(torch.equal(vals[:, :L].reshape(n_inst, N, L), shards[:n_inst, :, :L])))
+    ms_w, ms_r, ms_v = timed(write, reps), timed(read, reps), timed(validate, reps)
+    value_bytes = m * L
+    return {"workload": f"{m} Message::Value(proof) of {n_inst} N={N} instances (1 MiB proposals)",
+            "msg_bytes": total, "write_ms": ms_w, "read_ms": ms_r, "validate_ms": ms_v,
+            "write_hbm_GBps": (value_bytes + total) / (ms_w * 1e-3) / 1e9,
+            "read_hbm_GBps": (total + value_bytes) / (ms_r * 1e-3) / 1e9,
+            "hbm_frac_write": (value_bytes + total) / (ms_w * 1e-3) / HBM_PEAK,
+            "hbm_frac_read": (total + value_bytes) / (ms_r * 1e-3) / HBM_PEAK,
+            "validate_proofs_per_s": m / (ms_v * 1e-3), "roundtrip_ok": good}
+
+
 def network_leg(ctx, dev, n_nodes: int, reps: int):
     """configs[4]: the RBC half of one epoch of ONE n_nodes-node network whose
     nodes are split over all ranks (hydrabadger_amd/network.py): encode the
@@ -516,6 +573,10 @@ def main():
         decode = {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
                   "erased_per_instance": parity, "roundtrip_ok": ok}
 
+    bwire = None
+    if a.wire_instances > 0:
+        bwire = broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps)
+
     epoch = None
     if a.epoch_nodes > 0 and a.epoch_nodes % world == 0:
         epoch = network_leg(ctx, dev, a.epoch_nodes, max(2, min(a.steps, 5)))
@@ -551,6 +612,7 @@ def main():
             "shard_bytes_GBps": value * N_NODES * L / PAYLOAD,
             "tdec": tdec,
             "network_epoch": epoch,
+            "broadcast_wire": bwire,
             "wire_signatures": wire,
             "tdec_inputs": tdec_in,
             "coin": coin,

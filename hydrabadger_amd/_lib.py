@@ -30,6 +30,10 @@ HBG_E_SINGULAR_MATRIX = -17
 HBG_E_NOT_ENOUGH_SHARES = -20
 HBG_E_DUPLICATE_ENTRY = -21
 HBG_E_INVALID_POINT = -22
+HBG_E_WIRE_EOF = -30
+HBG_E_WIRE_TAG = -31
+
+HBG_MSG_VALUE, HBG_MSG_ECHO, HBG_MSG_READY, HBG_MSG_CAN_DECODE, HBG_MSG_ECHO_HASH = 0, 1, 2, 3, 4
 
 HBG_DEVICE = 1
 HBG_ASYNC = 2
@@ -58,6 +62,11 @@ SIGNATURES = {
     "hbg_merkle_validate": (_i, [_vp, _u32, _u64, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u8p, _u64, _u32]),
     "hbg_rbc_encode_merkle": (_i, [_vp, _u32, _u8p, _u64, _vp, _u64, _u8p, _u64, _u8p, _u64, _u32]),
     "hbg_rbc_decode": (_i, [_vp, _u32, _u64, _u8p, _u64, _u8p, _u8p, _u8p, _u64, _vp, _u8p, _u64, _u32]),
+    "hbg_proof_digests": (_u32, [_u32, _u32]),
+    "hbg_proof_msg_len": (_u64, [_u32, _u32, _u64]),
+    "hbg_rbc_write_proof_msgs": (_i, [_vp, _u32, _u64, _u8p, _u64, _u8p, _u64, _u32, _u64, _vp, _vp, _u8p, _vp,
+                                      _u32]),
+    "hbg_rbc_read_msgs": (_i, [_vp, _u32, _u64, _u8p, _vp, _u64, _vp, _u8p, _u64, _vp, _u8p, _vp, _u8p, _vp, _u32]),
     "hbg_synth_bytes": (_i, [_vp, _u32, _u64, _u64, _u8p, _u64, _u64, _u32]),
     "hbg_tdec_verify_shares": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_ct_verify": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u32]),

@@ -395,3 +395,127 @@ def synth_bytes(tag: int, first_instance: int, nbytes: int, out, ctx: _lib.Conte
     flags = (_lib.HBG_DEVICE if device else 0) | (_lib.HBG_ASYNC if asynchronous else 0)
     h = (ctx or default_context()).h
     check(lib().hbg_synth_bytes(h, tag, first_instance, nbytes, ptr(out), out.shape[-1], n, flags), "synth_bytes")
+
+
+# ----------------------------------------------------------------------------- wire format
+@dataclass
+class Message:
+    """hbbft ``broadcast::Message``: ``kind`` is the bincode variant index
+    (VALUE/ECHO carry a ``Proof``, READY/CAN_DECODE/ECHO_HASH a digest)."""
+
+    VALUE, ECHO, READY, CAN_DECODE, ECHO_HASH = (_lib.HBG_MSG_VALUE, _lib.HBG_MSG_ECHO, _lib.HBG_MSG_READY,
+                                                 _lib.HBG_MSG_CAN_DECODE, _lib.HBG_MSG_ECHO_HASH)
+    kind: int
+    payload: object  # Proof or 32-byte digest
+
+    @classmethod
+    def value(cls, proof: Proof) -> "Message":
+        return cls(cls.VALUE, proof)
+
+    @classmethod
+    def echo(cls, proof: Proof) -> "Message":
+        return cls(cls.ECHO, proof)
+
+    @classmethod
+    def ready(cls, digest: bytes) -> "Message":
+        return cls(cls.READY, bytes(digest))
+
+
+class WireError(HbgError):
+    """bincode::Error of a broadcast message (UnexpectedEof / InvalidVariant)."""
+
+
+def proof_msg_len(n: int, index: int, shard_len: int) -> int:
+    return int(lib().hbg_proof_msg_len(n, index, shard_len))
+
+
+def proof_msg_offsets(n: int, shard_len: int, index) -> np.ndarray:
+    """out_off [m+1] (u64) for Value/Echo messages of leaves ``index`` laid end to end."""
+    index = np.asarray(index, np.int64)
+    lens = np.array([proof_msg_len(n, int(i), shard_len) for i in range(n)], np.uint64)
+    off = np.zeros(index.shape[0] + 1, np.uint64)
+    off[1:] = np.cumsum(lens[index])
+    return off
+
+
+def write_proof_msgs_batch(n_nodes: int, shard_len: int, shards, levels, tag: int, inst, index, out, out_off,
+                           ctx: _lib.Context | None = None, device: bool = False, asynchronous: bool = False) -> None:
+    """bincode ``Message::{Value,Echo}(tree[inst[j]].proof(index[j]))`` for
+    every j, into out[out_off[j]:out_off[j+1]].  shards [n][N][S], levels
+    [n][nodes][32] as produced by ``rbc_encode_merkle_batch``; inst u64/int64,
+    index u32/int32, out_off u64/int64 [m+1]."""
+    flags = (_lib.HBG_DEVICE if device else 0) | (_lib.HBG_ASYNC if asynchronous else 0)
+    h = (ctx or default_context()).h
+    check(lib().hbg_rbc_write_proof_msgs(h, n_nodes, shard_len, ptr(shards), shards.shape[-1], ptr(levels),
+                                         shards.shape[0], tag, inst.shape[0], ptr(inst), ptr(index), ptr(out),
+                                         ptr(out_off), flags), "write_proof_msgs")
+
+
+def read_msgs_batch(n_nodes: int, shard_len: int, msgs, msg_off, tag, values, index, digests, ndigests, roots,
+                    status, ctx: _lib.Context | None = None, device: bool = False,
+                    asynchronous: bool = False) -> None:
+    """``bincode::deserialize::<Message>`` of m messages (msgs[msg_off[j]:
+    msg_off[j+1]]) into the ``validate_proofs`` table: tag/index/ndigests u32
+    [m], values [m][S], digests [m][depth][32], roots [m][32], status i32 [m]."""
+    m = msg_off.shape[0] - 1
+    flags = (_lib.HBG_DEVICE if device else 0) | (_lib.HBG_ASYNC if asynchronous else 0)
+    h = (ctx or default_context()).h
+    check(lib().hbg_rbc_read_msgs(h, n_nodes, shard_len, ptr(msgs), ptr(msg_off), m, ptr(tag), ptr(values),
+                                  values.shape[-1], ptr(index), ptr(digests), ptr(ndigests), ptr(roots), ptr(status),
+                                  flags), "read_msgs")
+
+
+def serialize_proof_messages(tree: MerkleTree, tag: int, indices=None, ctx: _lib.Context | None = None) -> list:
+    """bincode of ``Message::Value/Echo(tree.proof(i))`` for each i (what
+    ``Broadcast::send_shards`` hands to the transport), built on the GPU."""
+    vals = tree.values()
+    n = len(vals)
+    L = len(vals[0])
+    idx = np.arange(n, dtype=np.uint32) if indices is None else np.asarray(indices, np.uint32)
+    shards = np.zeros((1, n, max(L, 1)), np.uint8)
+    for i, v in enumerate(vals):
+        if L:
+            shards[0, i] = np.frombuffer(bytes(v), np.uint8)
+    levels = tree._flat.reshape(1, -1, 32)
+    off = proof_msg_offsets(n, L, idx)
+    out = np.zeros(max(int(off[-1]), 1), np.uint8)
+    inst = np.zeros(idx.shape[0], np.uint64)
+    write_proof_msgs_batch(n, L, shards, levels, tag, inst, idx, out, off, ctx)
+    return [out[int(off[j]):int(off[j + 1])].tobytes() for j in range(idx.shape[0])]
+
+
+def deserialize_messages(msgs: list, n: int, shard_len: int, ctx: _lib.Context | None = None) -> list:
+    """``bincode::deserialize::<Message>`` for each wire message of an n-node
+    broadcast with shards of shard_len bytes, on the GPU.  Returns a Message,
+    or raises-equivalent WireError objects in place of failed items (so a
+    batch keeps its order); a proof whose value is not shard_len bytes is
+    returned as WireError(HBG_E_INCORRECT_SHARD_SIZE)."""
+    m = len(msgs)
+    depth = max(_lib.merkle_depth(n), 1)
+    off = np.zeros(m + 1, np.uint64)
+    off[1:] = np.cumsum([len(b) for b in msgs]) if m else []
+    buf = np.frombuffer(b"".join(bytes(b) for b in msgs) or b"\0", np.uint8).copy()
+    S = max(shard_len, 1)
+    tag = np.zeros(m, np.uint32)
+    vals = np.zeros((m, S), np.uint8)
+    index = np.zeros(m, np.uint32)
+    dig = np.zeros((m, depth, 32), np.uint8)
+    nd = np.zeros(m, np.uint32)
+    roots = np.zeros((m, 32), np.uint8)
+    st = np.zeros(m, np.int32)
+    read_msgs_batch(n, shard_len, buf, off, tag, vals, index, dig, nd, roots, st, ctx)
+    res = []
+    for j in range(m):
+        if st[j] != 0:
+            res.append(WireError(int(st[j]), "bincode::deserialize"))
+        elif tag[j] >= Message.READY:
+            res.append(Message(int(tag[j]), roots[j].tobytes()))
+        else:
+            k = int(nd[j])
+            if k == 0xFFFFFFFF:  # more digests than an n-leaf proof has: carried as an unvalidatable marker
+                ds = [b"\0" * 32] * (_lib.merkle_depth(n) + 1)
+            else:
+                ds = [dig[j, q].tobytes() for q in range(k)]
+            res.append(Message(int(tag[j]), Proof(vals[j, :shard_len].tobytes(), int(index[j]), ds,
+                                                  roots[j].tobytes())))
+    return res

@@ -171,7 +171,7 @@ int encode_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shard
         HBG_TRY(launch_rs_encode_const(D, Q, shards, S, L, n, payloads, pstride, plen, c->stream));
         return HBG_OK;
     }
-    if (payloads) HBG_TRY(launch_pack_rows(shards, S, L, D, n, payloads, pstride, plen, c->stream));
+    if (payloads) HBG_TRY(launch_pack_rows(shards, S, L, D + Q, D, n, payloads, pstride, plen, c->stream));
     uint8_t* plan = nullptr;
     HBG_CHECK(device_encode_plan(c, D, Q, &plan));
     HBG_TRY(launch_rs_code_generic(shards, S, L, D + Q, D, n, plan, 0, c->stream));
@@ -217,6 +217,8 @@ const char* hbg_strerror(int code) {
         case HBG_E_NOT_ENOUGH_SHARES: return "NotEnoughShares";
         case HBG_E_DUPLICATE_ENTRY: return "DuplicateEntry";
         case HBG_E_INVALID_POINT: return "InvalidPoint";
+        case HBG_E_WIRE_EOF: return "UnexpectedEof";
+        case HBG_E_WIRE_TAG: return "InvalidVariant";
         default: return "unknown error";
     }
 }
@@ -416,7 +418,7 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
         if (Q) {
             HBG_CHECK(encode_device(c, D, Q, L, dsh, S, n, dpay, dps, dplen));
         } else {
-            HBG_TRY(launch_pack_rows(dsh, S, L, N, n, dpay, dps, dplen, c->stream));
+            HBG_TRY(launch_pack_rows(dsh, S, L, N, N, n, dpay, dps, dplen, c->stream));
         }
         HBG_TRY(launch_merkle_build(dsh, S, L, N, n, dlev, c->stream));
         return HBG_OK;
@@ -1088,6 +1090,103 @@ int hbg_test_bls(hbg_ctx* c, int op, uint32_t n, const uint32_t* in, uint32_t in
     HBG_TRY(bls::launch_tdec_test(op, n, (const uint32_t*)di, (uint32_t*)dout, in_words, out_words, (uint32_t*)dl,
                                   c->stream));
     HBG_TRY(hipMemcpyAsync(out, dout, 4ull * out_words * n, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+uint32_t hbg_proof_digests(uint32_t N, uint32_t index) { return host_proof_digests(N, index); }
+
+uint64_t hbg_proof_msg_len(uint32_t N, uint32_t index, uint64_t value_len) {
+    if (index >= N) return 0;
+    return 4 + 8 + value_len + 8 + 8 + 32ull * host_proof_digests(N, index) + 32;
+}
+
+int hbg_rbc_write_proof_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, uint64_t stride,
+                             const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m, const uint64_t* inst,
+                             const uint32_t* index, uint8_t* out, const uint64_t* out_off, uint32_t flags) {
+    if (!c || N == 0 || N > 256 || stride < L || tag > HBG_MSG_ECHO ||
+        (m && (!shards || !levels || !inst || !index || !out || !out_off || n == 0)))
+        return HBG_E_ARG;
+    if (m == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    if (flags & HBG_DEVICE) {
+        if (stride % 16 || !aligned(shards, 16) || !aligned(out, 16)) return HBG_E_ARG;
+        HBG_TRY(launch_rbc_write_proof_msgs(N, L, shards, stride, levels, n, tag, m, inst, index, out, out_off,
+                                           c->stream));
+        return finish(c, flags);
+    }
+    std::vector<uint64_t> off(m + 1);
+    for (uint64_t j = 0; j < m; ++j) {
+        if (index[j] >= N || inst[j] >= n || out_off[j + 1] < out_off[j] ||
+            out_off[j + 1] - out_off[j] != hbg_proof_msg_len(N, index[j], L))
+            return HBG_E_ARG;
+    }
+    for (uint64_t j = 0; j <= m; ++j) off[j] = out_off[j] - out_off[0];
+    const uint64_t S = round_up(L ? L : 1, 16), nodes = merkle_nodes(N), total = off[m];
+    void *dsh, *dlev, *dinst, *didx, *dout, *doff;
+    HBG_CHECK(scratch(c, 0, S * N * n, &dsh));
+    HBG_CHECK(scratch(c, 1, nodes * 32 * n, &dlev));
+    HBG_CHECK(scratch(c, 2, 8 * m, &dinst));
+    HBG_CHECK(scratch(c, 3, 4 * m, &didx));
+    HBG_CHECK(scratch(c, 4, total + 16, &dout));
+    HBG_CHECK(scratch(c, 5, 8 * (m + 1), &doff));
+    if (L) HBG_TRY(hipMemcpy2DAsync(dsh, S, shards, stride, L, (size_t)N * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dlev, levels, nodes * 32 * n, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(dinst, inst, 8 * m, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(didx, index, 4 * m, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(doff, off.data(), 8 * (m + 1), hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(launch_rbc_write_proof_msgs(N, L, (const uint8_t*)dsh, S, (const uint8_t*)dlev, n, tag, m,
+                                       (const uint64_t*)dinst, (const uint32_t*)didx, (uint8_t*)dout,
+                                       (const uint64_t*)doff, c->stream));
+    HBG_TRY(hipMemcpyAsync(out + out_off[0], dout, total, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_rbc_read_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* msgs, const uint64_t* msg_off, uint64_t m,
+                      uint32_t* tag, uint8_t* values, uint64_t vstride, uint32_t* index, uint8_t* digests,
+                      uint32_t* ndig, uint8_t* roots, int32_t* status, uint32_t flags) {
+    const uint32_t depth = merkle_depth(N);
+    if (!c || N == 0 || N > 256 || vstride < L ||
+        (m && (!msgs || !msg_off || !tag || !values || !index || !ndig || !roots || !status || (depth && !digests))))
+        return HBG_E_ARG;
+    if (m == 0) return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    if (flags & HBG_DEVICE) {
+        if (vstride % 16 || !aligned(values, 16)) return HBG_E_ARG;
+        HBG_TRY(launch_rbc_read_msgs(N, L, msgs, msg_off, m, tag, values, vstride, index, digests, ndig, roots,
+                                     status, c->stream));
+        return finish(c, flags);
+    }
+    std::vector<uint64_t> off(m + 1);
+    for (uint64_t j = 0; j < m; ++j)
+        if (msg_off[j + 1] < msg_off[j]) return HBG_E_ARG;
+    for (uint64_t j = 0; j <= m; ++j) off[j] = msg_off[j] - msg_off[0];
+    const uint64_t S = round_up(L ? L : 1, 16), total = off[m];
+    void *dmsg, *doff, *dtag, *dval, *didx, *ddig, *dnd, *drt, *dst;
+    HBG_CHECK(scratch(c, 0, total + 16, &dmsg));
+    HBG_CHECK(scratch(c, 1, 8 * (m + 1), &doff));
+    HBG_CHECK(scratch(c, 2, 4 * m, &dtag));
+    HBG_CHECK(scratch(c, 3, S * m, &dval));
+    HBG_CHECK(scratch(c, 4, 4 * m, &didx));
+    HBG_CHECK(scratch(c, 5, 32ull * depth * m + 16, &ddig));
+    HBG_CHECK(scratch(c, 6, 4 * m, &dnd));
+    HBG_CHECK(scratch(c, 7, 32 * m, &drt));
+    HBG_CHECK(scratch(c, 8, 4 * m, &dst));
+    if (total) HBG_TRY(hipMemcpyAsync(dmsg, msgs + msg_off[0], total, hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(hipMemcpyAsync(doff, off.data(), 8 * (m + 1), hipMemcpyHostToDevice, c->stream));
+    HBG_TRY(launch_rbc_read_msgs(N, L, (const uint8_t*)dmsg, (const uint64_t*)doff, m, (uint32_t*)dtag,
+                                 (uint8_t*)dval, S, (uint32_t*)didx, (uint8_t*)ddig, (uint32_t*)dnd, (uint8_t*)drt,
+                                 (int32_t*)dst, c->stream));
+    HBG_TRY(hipMemcpyAsync(tag, dtag, 4 * m, hipMemcpyDeviceToHost, c->stream));
+    if (L) HBG_TRY(hipMemcpy2DAsync(values, vstride, dval, S, L, m, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(index, didx, 4 * m, hipMemcpyDeviceToHost, c->stream));
+    if (depth) HBG_TRY(hipMemcpyAsync(digests, ddig, 32ull * depth * m, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(ndig, dnd, 4 * m, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(roots, drt, 32 * m, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipMemcpyAsync(status, dst, 4 * m, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipStreamSynchronize(c->stream));
     return HBG_OK;
 }

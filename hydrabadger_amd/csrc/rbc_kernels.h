@@ -59,7 +59,7 @@ inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
 bool has_const_encoder(uint32_t D, uint32_t Q);
 hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
-hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
+hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,
                             const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st);
@@ -74,6 +74,14 @@ hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* value
 hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                            const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
                            uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st);
+hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* shards, uint64_t S,
+                                       const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m,
+                                       const uint64_t* inst, const uint32_t* index, uint8_t* out,
+                                       const uint64_t* out_off, hipStream_t st);
+hipError_t launch_rbc_read_msgs(uint32_t N, uint64_t L, const uint8_t* msgs, const uint64_t* msg_off, uint64_t m,
+                                uint32_t* tag, uint8_t* values, uint64_t vstride, uint32_t* index,
+                                uint8_t* digests, uint32_t* ndig, uint8_t* roots, int32_t* status, hipStream_t st);
+uint32_t host_proof_digests(uint32_t N, uint32_t i);
 hipError_t launch_synth(uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride, uint64_t n,
                         hipStream_t st);
 

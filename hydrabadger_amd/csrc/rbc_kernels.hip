@@ -172,8 +172,10 @@ __global__ __launch_bounds__(256, 4) void rs_encode_const(uint8_t* __restrict__ 
 }
 
 // Pack only (Trivial coding, N <= 3): send_shards' buffer into N rows.
+// send_shards' prefix/pad/chunk into the first `rows` (= D) shards of each
+// N-shard instance (the parity rows are left to the coder).
 __global__ __launch_bounds__(256) void pack_rows(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint32_t N,
-                                                 uint64_t n, uint32_t blocks_per_inst,
+                                                 uint32_t rows, uint64_t n, uint32_t blocks_per_inst,
                                                  const uint8_t* __restrict__ payloads, uint64_t pstride,
                                                  const uint64_t* __restrict__ plen) {
     const uint64_t inst = blockIdx.x / blocks_per_inst;
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(256) void pack_rows(uint8_t* __restrict__ shards, u
     if (inst >= n || 4 * p >= L) return;
     const uint8_t* pay = payloads + inst * pstride;
     const uint64_t P = plen[inst];
-    for (uint32_t j = 0; j < N; ++j)
+    for (uint32_t j = 0; j < rows; ++j)
         reinterpret_cast<uint32_t*>(shards + (inst * N + j) * S)[p] = value_word(pay, P, (uint64_t)j * L + 4 * p);
 }
 
@@ -676,10 +678,11 @@ hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint6
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
+hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,
                             const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
-    pack_rows<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, payloads, pstride, plen);
+    pack_rows<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, rows, n, bpi, payloads, pstride,
+                                                               plen);
     return hipGetLastError();
 }
 

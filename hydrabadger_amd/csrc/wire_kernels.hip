@@ -1,0 +1,245 @@
+// wire_kernels.hip — SURVEY.md §8(f4): hbbft broadcast wire format on gfx950.
+//
+// bincode 1.x (default config: little-endian fixed-width integers, u64
+// sequence lengths, u32 enum variant index) of hbbft `broadcast::Message`
+// [EXT, VegeBun-csj/hbbft master, src/broadcast/message.rs]:
+//   Value(Proof<Vec<u8>>) = 0, Echo(Proof<Vec<u8>>) = 1, Ready(Digest) = 2,
+//   CanDecode(Digest) = 3, EchoHash(Digest) = 4
+// and `Proof<T> { value: T, index: usize, digests: Vec<Digest>, root_hash: Digest }`
+// [EXT, src/broadcast/merkle.rs]; `Digest = [u8; 32]` is a serde tuple (no
+// length).  A Value/Echo message for leaf i of an N-leaf tree is therefore
+//   u32 tag | u64 L | value[L] | u64 i | u64 k | k x digest[32] | root[32]
+// with k = hbg_proof_digests(N, i).  The reference builds these one at a time
+// in `Broadcast::send_shards` / `handle_value` (proof -> Message -> bincode in
+// hydrabadger's `WireMessages::start_send`, src/lib.rs:432-446) and parses
+// them in `WireMessages::poll` (src/lib.rs:397-404).
+//
+// Both kernels are HBM byte movers (no arithmetic): every thread owns one
+// 16-byte chunk of the destination, the value body is moved with aligned dword
+// loads + v_alignbyte and 16-B stores, header/trailer bytes (≤ 0.6 % of a
+// message at N=64, 1 MiB) go through a byte path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rbc_kernels.h"
+
+namespace hbg {
+
+__host__ __device__ inline uint32_t proof_digests(uint32_t N, uint32_t i) {
+    if (i >= N) return 0;
+    uint32_t k = 0, ln = N;
+    while (ln > 1) {
+        if ((i ^ 1u) < ln) ++k;
+        i >>= 1;
+        ln = (ln + 1) >> 1;
+    }
+    return k;
+}
+
+// flat-levels node of the j-th sibling digest of proof(i) (MerkleTree::proof's walk)
+__device__ inline uint32_t sibling_node(uint32_t N, uint32_t i, uint32_t j) {
+    uint32_t off = 0, ln = N, k = 0;
+    while (ln > 1) {
+        if ((i ^ 1u) < ln) {
+            if (k == j) return off + (i ^ 1u);
+            ++k;
+        }
+        off += ln;
+        i >>= 1;
+        ln = (ln + 1) >> 1;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ uint8_t le_byte(uint64_t v, uint32_t b) { return (uint8_t)(v >> (8 * b)); }
+
+// Byte o of message (tag, proof(inst, i)); value bytes come from the shard row.
+__device__ inline uint8_t proof_msg_byte(uint64_t o, uint32_t tag, uint64_t L, const uint8_t* __restrict__ row,
+                                         const uint8_t* __restrict__ lev, uint32_t nodes, uint32_t N, uint32_t i,
+                                         uint32_t k) {
+    if (o < 4) return le_byte(tag, (uint32_t)o);
+    if (o < 12) return le_byte(L, (uint32_t)(o - 4));
+    if (o < 12 + L) return row[o - 12];
+    const uint64_t t = o - 12 - L;
+    if (t < 8) return le_byte(i, (uint32_t)t);
+    if (t < 16) return le_byte(k, (uint32_t)(t - 8));
+    const uint64_t d = t - 16;
+    if (d < 32ull * k) return lev[(uint64_t)sibling_node(N, i, (uint32_t)(d >> 5)) * 32 + (d & 31)];
+    return lev[(uint64_t)(nodes - 1) * 32 + (d - 32ull * k)];
+}
+
+// 16 bytes starting at an arbitrary byte address p, from 4/5 aligned dwords.
+// Every dword read contains at least one byte of [p, p + 16).
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t* p) {
+    const uint32_t s = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+    uint32_t v[5];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = w[j];
+    v[4] = s ? w[4] : 0u;
+    uint4 r;
+    r.x = __builtin_amdgcn_alignbyte(v[1], v[0], s);
+    r.y = __builtin_amdgcn_alignbyte(v[2], v[1], s);
+    r.z = __builtin_amdgcn_alignbyte(v[3], v[2], s);
+    r.w = __builtin_amdgcn_alignbyte(v[4], v[3], s);
+    return r;
+}
+
+// grid: m messages x blocks_per_msg; thread = one 16-B destination chunk.
+__global__ __launch_bounds__(256) void rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* __restrict__ shards,
+                                                            uint64_t S, const uint8_t* __restrict__ levels,
+                                                            uint32_t nodes, uint64_t n, uint32_t tag, uint64_t m,
+                                                            const uint64_t* __restrict__ inst,
+                                                            const uint32_t* __restrict__ index,
+                                                            uint8_t* __restrict__ out,
+                                                            const uint64_t* __restrict__ out_off,
+                                                            uint32_t blocks_per_msg) {
+    const uint64_t j = blockIdx.x / blocks_per_msg;
+    if (j >= m) return;
+    const uint32_t i = index[j];
+    if (i >= N) return;
+    const uint32_t k = proof_digests(N, i);
+    const uint64_t start = out_off[j], end = out_off[j + 1];
+    if (end - start != 12 + L + 16 + 32ull * k + 32) return;  // layout mismatch: host mode rejects it up front
+    const uint64_t c = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 + threadIdx.x;
+    const uint64_t A = (start & ~15ull) + 16 * c;  // byte offset in out of this chunk
+    if (A >= end) return;
+    const uint64_t ki = inst[j];
+    if (ki >= n) return;
+    const uint8_t* row = shards + (ki * N + i) * S;
+    const uint8_t* lev = levels + ki * nodes * 32ull;
+    if (A >= start + 12 && A + 16 <= start + 12 + L) {  // interior of the value: 16-B move
+        const uint64_t s = A - start - 12;
+        *reinterpret_cast<uint4*>(out + A) = load16_unaligned(row + s);
+        return;
+    }
+    const uint64_t lo = A > start ? A : start, hi = A + 16 < end ? A + 16 : end;
+    for (uint64_t b = lo; b < hi; ++b) out[b] = proof_msg_byte(b - start, tag, L, row, lev, nodes, N, i, k);
+}
+
+__device__ __forceinline__ uint64_t rd_le(const uint8_t* p, int nb) {
+    uint64_t v = 0;
+    for (int b = 0; b < nb; ++b) v |= (uint64_t)p[b] << (8 * b);
+    return v;
+}
+
+// Parse message j: the bincode checks hbbft's deserialisation makes (EOF,
+// variant index) plus the layout this batch table can hold (value length ==
+// L).  Returns status; fills the header fields.
+struct MsgHdr {
+    int32_t status;
+    uint32_t tag;
+    uint64_t vlen, index, k, trailer;  // trailer = byte offset of the index field
+};
+
+__device__ inline MsgHdr parse_hdr(const uint8_t* __restrict__ msg, uint64_t len, uint64_t L) {
+    MsgHdr h{0, 0xFFFFFFFFu, 0, 0, 0, 0};
+    if (len < 4) {
+        h.status = HBG_E_WIRE_EOF;
+        return h;
+    }
+    h.tag = (uint32_t)rd_le(msg, 4);
+    if (h.tag > HBG_MSG_ECHO_HASH) {
+        h.status = HBG_E_WIRE_TAG;
+        return h;
+    }
+    if (h.tag >= HBG_MSG_READY) {
+        if (len < 36) h.status = HBG_E_WIRE_EOF;
+        return h;
+    }
+    if (len < 12) {
+        h.status = HBG_E_WIRE_EOF;
+        return h;
+    }
+    h.vlen = rd_le(msg + 4, 8);
+    if (h.vlen > len - 12 || len - 12 - h.vlen < 16) {
+        h.status = HBG_E_WIRE_EOF;
+        return h;
+    }
+    h.trailer = 12 + h.vlen;
+    h.index = rd_le(msg + h.trailer, 8);
+    h.k = rd_le(msg + h.trailer + 8, 8);
+    const uint64_t rest = len - h.trailer - 16;
+    if (h.k > rest / 32 || rest - 32 * h.k < 32) {
+        h.status = HBG_E_WIRE_EOF;
+        return h;
+    }
+    if (h.vlen != L) h.status = HBG_E_INCORRECT_SHARD_SIZE;
+    return h;
+}
+
+// grid: m messages x blocks_per_msg; thread = one 16-B chunk of the value row.
+__global__ __launch_bounds__(256) void rbc_read_msgs(uint64_t L, const uint8_t* __restrict__ msgs,
+                                                     const uint64_t* __restrict__ msg_off, uint64_t m,
+                                                     uint32_t* __restrict__ tag_out, uint8_t* __restrict__ values,
+                                                     uint64_t vstride, uint32_t* __restrict__ index_out,
+                                                     uint8_t* __restrict__ digests, uint32_t depth,
+                                                     uint32_t* __restrict__ ndig_out, uint8_t* __restrict__ roots,
+                                                     int32_t* __restrict__ status, uint32_t blocks_per_msg) {
+    const uint64_t j = blockIdx.x / blocks_per_msg;
+    if (j >= m) return;
+    const uint64_t start = msg_off[j], len = msg_off[j + 1] - start;
+    const uint8_t* msg = msgs + start;
+    const MsgHdr h = parse_hdr(msg, len, L);
+    const uint64_t c = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 + threadIdx.x;
+    if (c == 0) {
+        status[j] = h.status;
+        tag_out[j] = h.tag;
+        const bool proof = h.tag <= HBG_MSG_ECHO && (h.status == 0 || h.status == HBG_E_INCORRECT_SHARD_SIZE);
+        const bool digest = h.tag >= HBG_MSG_READY && h.tag <= HBG_MSG_ECHO_HASH && h.status == 0;
+        index_out[j] = proof ? (h.index > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)h.index) : 0u;
+        uint32_t nd = 0;
+        if (proof) nd = h.k > depth ? 0xFFFFFFFFu : (uint32_t)h.k;  // more than any valid proof: validate -> false
+        ndig_out[j] = nd;
+        uint8_t* rt = roots + j * 32;
+        if (proof) {
+            const uint8_t* src = msg + h.trailer + 16 + 32 * h.k;
+            for (int b = 0; b < 32; ++b) rt[b] = src[b];
+            if (nd != 0xFFFFFFFFu)
+                for (uint32_t b = 0; b < 32 * nd; ++b) digests[j * depth * 32ull + b] = msg[h.trailer + 16 + b];
+        } else if (digest) {
+            for (int b = 0; b < 32; ++b) rt[b] = msg[4 + b];
+        } else {
+            for (int b = 0; b < 32; ++b) rt[b] = 0;
+        }
+    }
+    if (h.status != 0 || h.tag > HBG_MSG_ECHO) return;
+    const uint64_t o = 16 * c;  // value byte offset of this chunk
+    if (o >= L) return;
+    uint8_t* dst = values + j * vstride + o;
+    const uint8_t* src = msg + 12 + o;
+    if (o + 16 <= L) {
+        *reinterpret_cast<uint4*>(dst) = load16_unaligned(src);
+        return;
+    }
+    for (uint64_t b = 0; o + b < L; ++b) dst[b] = src[b];
+}
+
+hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* shards, uint64_t S,
+                                       const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m,
+                                       const uint64_t* inst, const uint32_t* index, uint8_t* out,
+                                       const uint64_t* out_off, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    const uint64_t max_len = 12 + L + 16 + 32ull * merkle_depth(N) + 32;
+    const uint64_t chunks = max_len / 16 + 2;
+    const uint32_t bpm = (uint32_t)((chunks + 255) / 256);
+    hipLaunchKernelGGL(rbc_write_proof_msgs, dim3((uint32_t)(m * bpm)), dim3(256), 0, st, N, L, shards, S, levels,
+                       merkle_nodes(N), n, tag, m, inst, index, out, out_off, bpm);
+    return hipGetLastError();
+}
+
+hipError_t launch_rbc_read_msgs(uint32_t N, uint64_t L, const uint8_t* msgs, const uint64_t* msg_off, uint64_t m,
+                                uint32_t* tag, uint8_t* values, uint64_t vstride, uint32_t* index,
+                                uint8_t* digests, uint32_t* ndig, uint8_t* roots, int32_t* status,
+                                hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    const uint32_t bpm = (uint32_t)(((L + 15) / 16 + 255) / 256 + (L == 0 ? 1 : 0));
+    hipLaunchKernelGGL(rbc_read_msgs, dim3((uint32_t)(m * (bpm ? bpm : 1))), dim3(256), 0, st, L, msgs, msg_off,
+                       m, tag, values, vstride, index, digests, merkle_depth(N), ndig, roots, status,
+                       bpm ? bpm : 1u);
+    return hipGetLastError();
+}
+
+uint32_t host_proof_digests(uint32_t N, uint32_t i) { return proof_digests(N, i); }
+
+}  // namespace hbg

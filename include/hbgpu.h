@@ -55,6 +55,8 @@ extern "C" {
 #define HBG_E_NOT_ENOUGH_SHARES (-20)     /* threshold_crypto::Error::NotEnoughShares */
 #define HBG_E_DUPLICATE_ENTRY (-21)       /* threshold_crypto::Error::DuplicateEntry  */
 #define HBG_E_INVALID_POINT (-22)         /* bad compressed G1/G2 encoding            */
+#define HBG_E_WIRE_EOF (-30)              /* bincode::ErrorKind::Io(UnexpectedEof)    */
+#define HBG_E_WIRE_TAG (-31)              /* bincode: unknown enum variant index      */
 
 #define HBG_DEVICE 1u
 #define HBG_ASYNC 2u
@@ -238,6 +240,57 @@ int hbg_sig_combine(hbg_ctx *ctx, uint32_t t, uint64_t n, const uint8_t *share96
 int hbg_sig_verify_shares(hbg_ctx *ctx, uint32_t n_doc, const uint8_t *doc, const uint64_t *doc_off,
                           uint32_t n_pk, const uint8_t *pk48, uint64_t n, const uint8_t *share96,
                           const uint32_t *share_doc, const uint32_t *share_pk, uint8_t *ok, uint32_t flags);
+
+/* ---- hbbft broadcast wire format -----------------------
+ * bincode 1.x (default config: little-endian fixed-width integers, u64
+ * sequence lengths, u32 enum variant index, trailing bytes ignored) of hbbft
+ * broadcast::Message [EXT, src/broadcast/message.rs] — Value(Proof) = 0,
+ * Echo(Proof) = 1, Ready(Digest) = 2, CanDecode(Digest) = 3,
+ * EchoHash(Digest) = 4 — with Proof<Vec<u8>> {value, index: usize,
+ * digests: Vec<Digest>, root_hash} [EXT, src/broadcast/merkle.rs] and
+ * Digest = [u8; 32] (a tuple: no length).  A Value/Echo message for leaf i of
+ * an N-leaf tree is
+ *     u32 tag | u64 L | value[L] | u64 i | u64 k | k x [32] digests | [32] root
+ * with k = hbg_proof_digests(N, i).  The reference serialises / parses these
+ * one frame at a time in WireMessages::start_send / poll (src/lib.rs:432-446,
+ * src/lib.rs:397-404). */
+#define HBG_MSG_VALUE 0u
+#define HBG_MSG_ECHO 1u
+#define HBG_MSG_READY 2u
+#define HBG_MSG_CAN_DECODE 3u
+#define HBG_MSG_ECHO_HASH 4u
+
+uint32_t hbg_proof_digests(uint32_t N, uint32_t index);           /* k of proof(index); 0 if index >= N */
+uint64_t hbg_proof_msg_len(uint32_t N, uint32_t index, uint64_t value_len); /* bytes of Value/Echo(proof) */
+
+/* Message::{Value,Echo}(MerkleTree::proof(index[j])) of tree inst[j] for
+ * j < m, from a shard batch of n instances (the hbg_rbc_encode_merkle /
+ * hbg_merkle_build layout: shards, shard_stride, levels).  Message j is
+ * written to out[out_off[j] .. out_off[j+1]), which must be exactly
+ * hbg_proof_msg_len(N, index[j], shard_len) bytes (HBG_E_ARG otherwise in
+ * host mode; device mode leaves such a message unwritten).  tag is
+ * HBG_MSG_VALUE or HBG_MSG_ECHO.  Device mode needs shard_stride % 16 == 0 and
+ * 16-byte-aligned shards and out. */
+int hbg_rbc_write_proof_msgs(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, const uint8_t *shards,
+                             uint64_t shard_stride, const uint8_t *levels, uint64_t n, uint32_t tag,
+                             uint64_t m, const uint64_t *inst, const uint32_t *index, uint8_t *out,
+                             const uint64_t *out_off, uint32_t flags);
+
+/* bincode::deserialize::<Message>(msgs[msg_off[j] .. msg_off[j+1])) for j < m
+ * into the hbg_merkle_validate layout: tag[j]; for Value/Echo the value row
+ * (values + j*value_stride, shard_len bytes), index[j] (usize clamped to
+ * 0xFFFFFFFF), digests [m][hbg_merkle_depth(N)][32], ndigests[j] (0xFFFFFFFF
+ * when the proof carries more digests than any N-leaf proof: validate is then
+ * false, as in hbbft) and roots[j]; for Ready/CanDecode/EchoHash the digest in
+ * roots[j].  status[j] = 0, HBG_E_WIRE_EOF (truncated), HBG_E_WIRE_TAG
+ * (variant > 4) or HBG_E_INCORRECT_SHARD_SIZE (a well-formed proof whose value
+ * is not shard_len bytes: header fields are filled).  A value row is
+ * unspecified unless status[j] == 0 and tag[j] <= HBG_MSG_ECHO.
+ * Device mode needs value_stride % 16 == 0 and 16-byte-aligned values. */
+int hbg_rbc_read_msgs(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, const uint8_t *msgs,
+                      const uint64_t *msg_off, uint64_t m, uint32_t *tag, uint8_t *values,
+                      uint64_t value_stride, uint32_t *index, uint8_t *digests, uint32_t *ndigests,
+                      uint8_t *roots, int32_t *status, uint32_t flags);
 
 /* Device-side seeded generator: row k of out gets nbytes of
  * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */

@@ -265,7 +265,9 @@ def test_device_synth_matches_oracle():
         assert got[k, :61].tobytes() == synth.synth_bytes(1, 40 + k, 61)
 
 
-@pytest.mark.parametrize("N,P,n", [(16, 65536, 24), (64, 1 << 20, 6), (128, 1 << 20, 3), (4, 230, 100)])
+@pytest.mark.parametrize("N,P,n", [(16, 65536, 24), (64, 1 << 20, 6), (128, 1 << 20, 3), (4, 230, 100),
+                                   # (D, Q) without a compile-time encoder: pack_rows + rs_code_generic, n > 1
+                                   (5, 333, 40), (7, 1000, 9), (100, 5000, 3), (3, 50, 7)])
 def test_device_batch_encode_matches_oracle(N, P, n):
     pay, shards, levels, L, S = _device_batch(N, P, n, first=11)
     sh = shards.cpu().numpy()
