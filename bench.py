@@ -235,8 +235,14 @@ def wire_leg(ctx, dev, n_msgs: int, msg_len: int, reps: int):
     L = _lib.lib()
     flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
     g = torch.Generator(device="cpu").manual_seed(0x5167)
-    msgs = torch.randint(0, 256, (n_msgs * msg_len,), dtype=torch.uint8, generator=g).to(dev)
+    msgs = torch.randint(0, 256, (n_msgs, msg_len), dtype=torch.uint8, generator=g)
+    msgs[:, :4] = torch.tensor([7, 0, 0, 0], dtype=torch.uint8)  # WireMessageKind::Message: poll verifies it
+    msgs = msgs.reshape(-1).to(dev)
     off = (torch.arange(n_msgs + 1, dtype=torch.int64) * msg_len).to(dev)
+    flen = 4 + 8 + msg_len + 96
+    foff = (torch.arange(n_msgs + 1, dtype=torch.int64) * flen).to(dev)
+    frames = torch.empty(n_msgs * flen + 16, dtype=torch.uint8, device=dev)
+    fst = torch.empty(n_msgs, dtype=torch.int32, device=dev)
     n_keys = 64
     sk = _dev_scalars(n_keys, dev, 17)
     from oracle import bls12_381 as B  # checker only: public keys of the 64 signers
@@ -255,15 +261,31 @@ def wire_leg(ctx, dev, n_msgs: int, msg_len: int, reps: int):
     def verify():
         _lib.check(L.hbg_bls_verify(ctx.h, n_keys, pk.data_ptr(), n_msgs, who.data_ptr(), msgs.data_ptr(),
                                     off.data_ptr(), sig.data_ptr(), ok.data_ptr(), flags), "verify")
+    def sign_frames():  # §8(f4): WireMessages::start_send (sign + SignedWireMessage + codec frame)
+        _lib.check(L.hbg_wire_sign_frames(ctx.h, n_keys, sk.data_ptr(), n_msgs, who.data_ptr(), msgs.data_ptr(),
+                                          off.data_ptr(), frames.data_ptr(), foff.data_ptr(), flags), "sign_frames")
+
+    def poll_frames():  # WireMessages::poll (frame + bincode checks, kind, PublicKey::verify)
+        _lib.check(L.hbg_wire_verify_frames(ctx.h, n_keys, pk.data_ptr(), n_msgs, who.data_ptr(), frames.data_ptr(),
+                                            foff.data_ptr(), fst.data_ptr(), flags), "poll_frames")
     sign()
     verify()
+    sign_frames()
+    poll_frames()
     torch.cuda.synchronize()
     all_ok = bool(ok.all().item())
+    frames_ok = bool((fst == 0).all().item()) and bool(torch.equal(
+        frames[:n_msgs * flen].reshape(n_msgs, flen)[:, flen - 96:], sig))
     ms_s = timed(sign, reps)
     ms_v = timed(verify, reps)
+    ms_sf = timed(sign_frames, reps)
+    ms_pf = timed(poll_frames, reps)
     return {"workload": f"{n_msgs} wire messages x {msg_len} B, 64 signers (SecretKey::sign / PublicKey::verify)",
             "sign_per_s": n_msgs / (ms_s * 1e-3), "verify_per_s": n_msgs / (ms_v * 1e-3), "sign_ms": ms_s,
-            "verify_ms": ms_v, "all_verified": all_ok}
+            "verify_ms": ms_v, "all_verified": all_ok,
+            "frames": {"workload": "WireMessages::start_send / poll: SignedWireMessage in LengthDelimitedCodec frames",
+                       "sign_frames_per_s": n_msgs / (ms_sf * 1e-3), "poll_frames_per_s": n_msgs / (ms_pf * 1e-3),
+                       "sign_frames_ms": ms_sf, "poll_frames_ms": ms_pf, "all_accepted": frames_ok}}
 
 
 def tdec_inputs_leg(ctx, dev, n_ct: int, n_nodes: int, reps: int):

@@ -32,6 +32,10 @@ HBG_E_DUPLICATE_ENTRY = -21
 HBG_E_INVALID_POINT = -22
 HBG_E_WIRE_EOF = -30
 HBG_E_WIRE_TAG = -31
+HBG_E_WIRE_FRAME = -32
+HBG_E_INVALID_SIGNATURE = -33
+HBG_E_UNKNOWN_PEER = -34
+HBG_WIRE_KIND_MESSAGE, HBG_WIRE_KIND_KEYGEN, HBG_WIRE_KIND_MAX = 7, 9, 10
 
 HBG_MSG_VALUE, HBG_MSG_ECHO, HBG_MSG_READY, HBG_MSG_CAN_DECODE, HBG_MSG_ECHO_HASH = 0, 1, 2, 3, 4
 
@@ -67,6 +71,9 @@ SIGNATURES = {
     "hbg_rbc_write_proof_msgs": (_i, [_vp, _u32, _u64, _u8p, _u64, _u8p, _u64, _u32, _u64, _vp, _vp, _u8p, _vp,
                                       _u32]),
     "hbg_rbc_read_msgs": (_i, [_vp, _u32, _u64, _u8p, _vp, _u64, _vp, _u8p, _u64, _vp, _u8p, _vp, _u8p, _vp, _u32]),
+    "hbg_wire_frame_len": (_u64, [_u64]),
+    "hbg_wire_sign_frames": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _u8p, _vp, _u32]),
+    "hbg_wire_verify_frames": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _vp, _u32]),
     "hbg_synth_bytes": (_i, [_vp, _u32, _u64, _u64, _u8p, _u64, _u64, _u32]),
     "hbg_tdec_verify_shares": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_ct_verify": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u32]),

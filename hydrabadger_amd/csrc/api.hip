@@ -219,6 +219,9 @@ const char* hbg_strerror(int code) {
         case HBG_E_INVALID_POINT: return "InvalidPoint";
         case HBG_E_WIRE_EOF: return "UnexpectedEof";
         case HBG_E_WIRE_TAG: return "InvalidVariant";
+        case HBG_E_WIRE_FRAME: return "FrameLength";
+        case HBG_E_INVALID_SIGNATURE: return "InvalidSignature";
+        case HBG_E_UNKNOWN_PEER: return "VerificationMessageReceivedUnknownPeer";
         default: return "unknown error";
     }
 }
@@ -1189,6 +1192,104 @@ int hbg_rbc_read_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* msgs, c
     HBG_TRY(hipMemcpyAsync(status, dst, 4 * m, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipStreamSynchronize(c->stream));
     return HBG_OK;
+}
+
+uint64_t hbg_wire_frame_len(uint64_t msg_len) { return 4 + 8 + msg_len + 96; }
+
+int hbg_wire_sign_frames(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_t n, const uint32_t* msg_sk,
+                         const uint8_t* msg, const uint64_t* msg_off, uint8_t* frames, const uint64_t* frame_off,
+                         uint32_t flags) {
+    if (!c || (n && (!sk32 || !msg_sk || !msg_off || !frames || !frame_off || n_sk == 0))) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!index_ok(flags, msg_sk, n, n_sk)) return HBG_E_ARG;
+    uint64_t max_len = 0;
+    if (!(flags & HBG_DEVICE)) {
+        for (uint64_t k = 0; k < n; ++k) {
+            if (msg_off[k + 1] < msg_off[k] || frame_off[k + 1] < frame_off[k]) return HBG_E_ARG;
+            const uint64_t len = msg_off[k + 1] - msg_off[k];
+            if (frame_off[k + 1] - frame_off[k] != hbg_wire_frame_len(len)) return HBG_E_ARG;
+            if (len > max_len) max_len = len;
+        }
+        if (msg_off[n] && !msg) return HBG_E_ARG;
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
+    const uint64_t flen = (flags & HBG_DEVICE) ? 0 : frame_off[n] - frame_off[0];
+    const void *dsk, *dms, *dm, *doff;
+    void *dsig, *dfr, *dfo;
+    HBG_CHECK(stage_in(c, flags, 0, sk32, 32ull * n_sk, &dsk));
+    HBG_CHECK(stage_in(c, flags, 1, msg_sk, 4ull * n, &dms));
+    HBG_CHECK(stage_in(c, flags, 2, msg, mlen, &dm));
+    HBG_CHECK(stage_in(c, flags, 3, msg_off, 8ull * (n + 1), &doff));
+    HBG_CHECK(scratch(c, 4, 96ull * n, &dsig));
+    const uint64_t* dfoff;
+    if (flags & HBG_DEVICE) {
+        dfr = frames;
+        dfoff = frame_off;
+        // frame sizes are the caller's contract in device mode (the pack kernel skips frames of the
+        // wrong size); the grid is sized for the longest message, read from the (small) offsets
+        std::vector<uint64_t> h(n + 1);
+        HBG_TRY(hipMemcpyAsync(h.data(), msg_off, 8ull * (n + 1), hipMemcpyDeviceToHost, c->stream));
+        HBG_TRY(hipStreamSynchronize(c->stream));
+        for (uint64_t k = 0; k < n; ++k)
+            if (h[k + 1] > h[k] && h[k + 1] - h[k] > max_len) max_len = h[k + 1] - h[k];
+    } else {
+        std::vector<uint64_t> off(n + 1);
+        for (uint64_t k = 0; k <= n; ++k) off[k] = frame_off[k] - frame_off[0];
+        HBG_CHECK(scratch(c, 5, flen + 16, &dfr));
+        HBG_CHECK(scratch(c, 6, 8ull * (n + 1), &dfo));
+        HBG_TRY(hipMemcpyAsync(dfo, off.data(), 8ull * (n + 1), hipMemcpyHostToDevice, c->stream));
+        dfoff = (const uint64_t*)dfo;
+    }
+    HBG_TRY(bls::launch_bls_sign(n, (const uint8_t*)dsk, (const uint32_t*)dms, (const uint8_t*)dm,
+                                 (const uint64_t*)doff, (uint8_t*)dsig, c->stream));
+    HBG_TRY(launch_wire_frame_pack(n, (const uint8_t*)dm, (const uint64_t*)doff, (const uint8_t*)dsig,
+                                   (uint8_t*)dfr, dfoff, max_len, c->stream));
+    if (flags & HBG_DEVICE) return finish(c, flags);
+    HBG_TRY(hipMemcpyAsync(frames + frame_off[0], dfr, flen, hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    return HBG_OK;
+}
+
+int hbg_wire_verify_frames(hbg_ctx* c, uint32_t n_pk, const uint8_t* pk48, uint64_t n, const uint32_t* frame_pk,
+                           const uint8_t* frames, const uint64_t* frame_off, int32_t* status, uint32_t flags) {
+    if (!c || (n && (!frame_pk || !frames || !frame_off || !status)) || (n_pk && !pk48)) return HBG_E_ARG;
+    if (n == 0) return HBG_OK;
+    if (!(flags & HBG_DEVICE))
+        for (uint64_t k = 0; k < n; ++k)
+            if (frame_off[k + 1] < frame_off[k]) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    const uint64_t flen = (flags & HBG_DEVICE) ? 0 : frame_off[n] - frame_off[0];
+    const void *dpk, *dfp, *dfr, *dfo;
+    void *dst, *paff, *pst, *lines;
+    std::vector<uint64_t> off;
+    if (flags & HBG_DEVICE) {
+        dfr = frames;
+        dfo = frame_off;
+    } else {
+        off.resize(n + 1);
+        for (uint64_t k = 0; k <= n; ++k) off[k] = frame_off[k] - frame_off[0];
+        HBG_CHECK(stage_in(c, flags, 2, frames + frame_off[0], flen, &dfr));
+        HBG_CHECK(stage_in(c, flags, 3, off.data(), 8ull * (n + 1), &dfo));
+    }
+    HBG_CHECK(stage_in(c, flags, 0, pk48, 48ull * (n_pk ? n_pk : 1), &dpk));
+    HBG_CHECK(stage_in(c, flags, 1, frame_pk, 4ull * n, &dfp));
+    HBG_CHECK(stage_out(c, flags, 4, status, 4ull * n, &dst));
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * (n_pk ? n_pk : 1), &paff));
+    HBG_CHECK(scratch(c, 13, 4ull * (n_pk ? n_pk : 1), &pst));
+    const uint64_t chunk = n < kVerifyChunk ? n : kVerifyChunk;
+    HBG_CHECK(scratch(c, 6, 8ull * bls::kLineWordsPerPoint * chunk, &lines));
+    if (n_pk) HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+        const uint64_t m = (n - k0) < chunk ? (n - k0) : chunk;
+        HBG_TRY(bls::launch_wire_verify_frames(m, (const uint32_t*)paff, (const int32_t*)pst, n_pk,
+                                               (const uint32_t*)dfp + k0, (const uint8_t*)dfr,
+                                               (const uint64_t*)dfo + k0, (uint32_t*)lines, (int32_t*)dst + k0,
+                                               c->stream));
+    }
+    return drain(c, flags, {{status, {dst, 4ull * n}}});
 }
 
 int hbg_synth_bytes(hbg_ctx* c, uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride,

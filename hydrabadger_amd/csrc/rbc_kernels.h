@@ -82,6 +82,8 @@ hipError_t launch_rbc_read_msgs(uint32_t N, uint64_t L, const uint8_t* msgs, con
                                 uint32_t* tag, uint8_t* values, uint64_t vstride, uint32_t* index,
                                 uint8_t* digests, uint32_t* ndig, uint8_t* roots, int32_t* status, hipStream_t st);
 uint32_t host_proof_digests(uint32_t N, uint32_t i);
+hipError_t launch_wire_frame_pack(uint64_t n, const uint8_t* msg, const uint64_t* msg_off, const uint8_t* sig96,
+                                  uint8_t* frames, const uint64_t* frame_off, uint64_t max_len, hipStream_t st);
 hipError_t launch_synth(uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride, uint64_t n,
                         hipStream_t st);
 

@@ -44,6 +44,9 @@ hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, con
                                    hipStream_t st);
 hipError_t launch_bls_sign(uint64_t n, const uint8_t* sk32, const uint32_t* msg_sk, const uint8_t* msg,
                            const uint64_t* off, uint8_t* sig96, hipStream_t st);
+hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
+                                     const uint32_t* frame_pk, const uint8_t* frames, const uint64_t* off,
+                                     uint32_t* lines, int32_t* status, hipStream_t st);
 hipError_t launch_bls_verify(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* msg_pk,
                              const uint8_t* msg, const uint64_t* off, const uint8_t* sig96, uint32_t* lines,
                              uint8_t* ok, hipStream_t st);

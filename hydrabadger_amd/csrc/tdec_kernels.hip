@@ -1024,6 +1024,64 @@ TDEC_KERNEL void bls_verify(uint64_t n, const uint32_t* __restrict__ pk_aff, con
     ok[k] = good ? 1 : 0;
 }
 
+// WireMessages::poll (src/lib.rs:397-420) for one length-delimited frame:
+// LengthDelimitedCodec's BE u32 length == frame body, bincode SignedWireMessage
+// { message: Vec<u8> (u64 LE len), sig: Signature (96-B compressed G2 tuple) }
+// with the crate's point check, then the WireMessage kind (bincode u32 variant
+// of WireMessageKind, src/lib.rs:250-270) and, for Message (7) / KeyGen (9)
+// only, PublicKey::verify(sig, message) with the peer's key.
+__device__ __forceinline__ uint64_t wire_le(const uint8_t* p, int nb) {
+    uint64_t v = 0;
+    for (int b = 0; b < nb; ++b) v |= (uint64_t)p[b] << (8 * b);
+    return v;
+}
+
+TDEC_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_aff,
+                                    const int32_t* __restrict__ pk_status, uint32_t n_pk,
+                                    const uint32_t* __restrict__ frame_pk, const uint8_t* __restrict__ frames,
+                                    const uint64_t* __restrict__ off, uint32_t* __restrict__ lines,
+                                    int32_t* __restrict__ status) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint8_t* f = frames + off[k];
+    const uint64_t flen = off[k + 1] - off[k];
+    int32_t st = HBG_OK;
+    uint64_t mlen = 0;
+    G2A sig;
+    if (flen < 4) st = HBG_E_WIRE_EOF;
+    else if (((uint64_t)f[0] << 24 | (uint64_t)f[1] << 16 | (uint64_t)f[2] << 8 | f[3]) != flen - 4)
+        st = HBG_E_WIRE_FRAME;
+    else if (flen - 4 < 8) st = HBG_E_WIRE_EOF;
+    else {
+        mlen = wire_le(f + 4, 8);
+        if (mlen > flen - 12 || flen - 12 - mlen < 96) st = HBG_E_WIRE_EOF;
+        else if (!g2_decompress(f + 12 + mlen, sig, true)) st = HBG_E_INVALID_POINT;
+        else if (mlen < 4) st = HBG_E_WIRE_EOF;
+        else {
+            const uint32_t kind = (uint32_t)wire_le(f + 12, 4);
+            if (kind > HBG_WIRE_KIND_MAX) st = HBG_E_WIRE_TAG;
+            else if (kind == HBG_WIRE_KIND_MESSAGE || kind == HBG_WIRE_KIND_KEYGEN) {
+                const uint32_t p = frame_pk[k];
+                if (p >= n_pk || pk_status[p] != 0) st = HBG_E_UNKNOWN_PEER;
+            }
+        }
+    }
+    const bool check = st == HBG_OK && (wire_le(f + 12, 4) == HBG_WIRE_KIND_MESSAGE ||
+                                        wire_le(f + 12, 4) == HBG_WIRE_KIND_KEYGEN);
+    if (check) {
+        const G2A h = hash_g2_msg(f + 12, (uint32_t)mlen);
+        uint32_t* lh = lines + k * 2ull * kLineWordsPerPoint;
+        uint32_t* ls = lh + kLineWordsPerPoint;
+        g2_prepare(h.x, h.y, lh);
+        if (!sig.inf) g2_prepare(sig.x, sig.y, ls);
+        const uint32_t* pa = pk_aff + 32ull * frame_pk[k];
+        if (!pairing_check2(lh, load_fp(pa), load_fp(pa + 12), pa[24] == 0, ls, fp_const(kG1x),
+                            fp_neg(fp_const(kG1y)), !sig.inf))
+            st = HBG_E_INVALID_SIGNATURE;
+    }
+    status[k] = st;
+}
+
 // PublicKey::encrypt_with_rng with r explicit: U = r G1, V = xor_with_hash(r PK, msg),
 // W = r hash_g1_g2(U, V).  V is written at the message's offsets.
 TDEC_KERNEL void tdec_encrypt(uint64_t n, const uint32_t* __restrict__ pk_aff, const uint8_t* __restrict__ r32,
@@ -1538,6 +1596,14 @@ hipError_t launch_bls_verify(uint64_t n, const uint32_t* pk_aff, const int32_t* 
                              uint8_t* ok, hipStream_t st) {
     if (n == 0) return hipSuccess;
     bls_verify<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok);
+    return hipGetLastError();
+}
+hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
+                                     const uint32_t* frame_pk, const uint8_t* frames, const uint64_t* off,
+                                     uint32_t* lines, int32_t* status, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    wire_verify_frames<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, n_pk, frame_pk, frames, off, lines,
+                                                       status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const uint8_t* r32, const uint8_t* msg,

@@ -215,6 +215,50 @@ __global__ __launch_bounds__(256) void rbc_read_msgs(uint64_t L, const uint8_t* 
     for (uint64_t b = 0; o + b < L; ++b) dst[b] = src[b];
 }
 
+// WireMessages::start_send framing: u32 BE (8 + len + 96) | u64 LE len |
+// message | sig96 (sig from bls_sign into a [n][96] table).  grid: n frames x
+// blocks_per_frame; thread = one 16-B destination chunk, as above.
+__global__ __launch_bounds__(256) void wire_frame_pack(uint64_t n, const uint8_t* __restrict__ msg,
+                                                       const uint64_t* __restrict__ msg_off,
+                                                       const uint8_t* __restrict__ sig96, uint8_t* __restrict__ frames,
+                                                       const uint64_t* __restrict__ frame_off,
+                                                       uint32_t blocks_per_frame) {
+    const uint64_t k = blockIdx.x / blocks_per_frame;
+    if (k >= n) return;
+    const uint64_t len = msg_off[k + 1] - msg_off[k];
+    const uint64_t start = frame_off[k], end = frame_off[k + 1];
+    if (end - start != 12 + len + 96) return;
+    const uint64_t c = (uint64_t)(blockIdx.x % blocks_per_frame) * 256 + threadIdx.x;
+    const uint64_t A = (start & ~15ull) + 16 * c;
+    if (A >= end) return;
+    const uint8_t* m = msg + msg_off[k];
+    if (A >= start + 12 && A + 16 <= start + 12 + len) {
+        *reinterpret_cast<uint4*>(frames + A) = load16_unaligned(m + (A - start - 12));
+        return;
+    }
+    const uint64_t lo = A > start ? A : start, hi = A + 16 < end ? A + 16 : end;
+    const uint64_t body = 8 + len + 96;
+    for (uint64_t b = lo; b < hi; ++b) {
+        const uint64_t o = b - start;
+        uint8_t v;
+        if (o < 4) v = (uint8_t)(body >> (8 * (3 - o)));
+        else if (o < 12) v = le_byte(len, (uint32_t)(o - 4));
+        else if (o < 12 + len) v = m[o - 12];
+        else v = sig96[96 * k + (o - 12 - len)];
+        frames[b] = v;
+    }
+}
+
+hipError_t launch_wire_frame_pack(uint64_t n, const uint8_t* msg, const uint64_t* msg_off, const uint8_t* sig96,
+                                  uint8_t* frames, const uint64_t* frame_off, uint64_t max_len, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t chunks = (12 + max_len + 96) / 16 + 2;
+    const uint32_t bpf = (uint32_t)((chunks + 255) / 256);
+    hipLaunchKernelGGL(wire_frame_pack, dim3((uint32_t)(n * bpf)), dim3(256), 0, st, n, msg, msg_off, sig96, frames,
+                       frame_off, bpf);
+    return hipGetLastError();
+}
+
 hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* shards, uint64_t S,
                                        const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m,
                                        const uint64_t* inst, const uint32_t* index, uint8_t* out,

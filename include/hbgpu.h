@@ -57,6 +57,9 @@ extern "C" {
 #define HBG_E_INVALID_POINT (-22)         /* bad compressed G1/G2 encoding            */
 #define HBG_E_WIRE_EOF (-30)              /* bincode::ErrorKind::Io(UnexpectedEof)    */
 #define HBG_E_WIRE_TAG (-31)              /* bincode: unknown enum variant index      */
+#define HBG_E_WIRE_FRAME (-32)            /* length-delimited prefix != frame body    */
+#define HBG_E_INVALID_SIGNATURE (-33)     /* hydrabadger Error::InvalidSignature      */
+#define HBG_E_UNKNOWN_PEER (-34)          /* Error::VerificationMessageReceivedUnknownPeer */
 
 #define HBG_DEVICE 1u
 #define HBG_ASYNC 2u
@@ -291,6 +294,43 @@ int hbg_rbc_read_msgs(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, const uint8_
                       const uint64_t *msg_off, uint64_t m, uint32_t *tag, uint8_t *values,
                       uint64_t value_stride, uint32_t *index, uint8_t *digests, uint32_t *ndigests,
                       uint8_t *roots, int32_t *status, uint32_t flags);
+
+/* ---- §8(f4) + §8(f2): hydrabadger's signed, length-delimited frames -------
+ * WireMessages (src/lib.rs:358-447) sends every serialised WireMessage as
+ *     u32 BE body_len | bincode SignedWireMessage { message: Vec<u8>, sig }
+ *   = u32 BE (8 + len + 96) | u64 LE len | message[len] | sig[96]
+ * (tokio LengthDelimitedCodec default: 4-byte big-endian length; Signature =
+ * 96-byte compressed G2 tuple) and, on receipt, verifies the signature only
+ * for WireMessageKind::Message and ::KeyGen (bincode variants 7 and 9 of the
+ * 11 at src/lib.rs:250-270: the message's first 4 bytes, u32 LE). */
+#define HBG_WIRE_KIND_MESSAGE 7u
+#define HBG_WIRE_KIND_KEYGEN 9u
+#define HBG_WIRE_KIND_MAX 10u
+
+uint64_t hbg_wire_frame_len(uint64_t msg_len); /* 4 + 8 + msg_len + 96 */
+
+/* WireMessages::start_send for n serialised WireMessages: message k
+ * (msg[msg_off[k] .. msg_off[k+1]]) signed with sk32[msg_sk[k]]
+ * (SecretKey::sign, src/lib.rs:434) and framed into
+ * frames[frame_off[k] .. frame_off[k+1]] (exactly hbg_wire_frame_len bytes:
+ * HBG_E_ARG otherwise in host mode; device mode leaves such a frame
+ * unwritten). */
+int hbg_wire_sign_frames(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint64_t n,
+                         const uint32_t *msg_sk, const uint8_t *msg, const uint64_t *msg_off,
+                         uint8_t *frames, const uint64_t *frame_off, uint32_t flags);
+
+/* WireMessages::poll for n received frames (frames[frame_off[k] ..
+ * frame_off[k+1]], each one codec frame incl. its 4-byte prefix) from peers
+ * whose public keys are pk48[frame_pk[k]] (frame_pk[k] >= n_pk: peer key
+ * unknown).  status[k] = 0 (the frame yields its WireMessage: verified, or a
+ * kind the reference does not verify), HBG_E_WIRE_FRAME, HBG_E_WIRE_EOF,
+ * HBG_E_INVALID_POINT (sig does not deserialise), HBG_E_WIRE_TAG (kind > 10),
+ * HBG_E_UNKNOWN_PEER or HBG_E_INVALID_SIGNATURE.  The message of frame k is
+ * frames[frame_off[k] + 12 ..][..len].  Beyond the kind index the inner
+ * WireMessage is not deserialised (control plane). */
+int hbg_wire_verify_frames(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
+                           const uint32_t *frame_pk, const uint8_t *frames, const uint64_t *frame_off,
+                           int32_t *status, uint32_t flags);
 
 /* Device-side seeded generator: row k of out gets nbytes of
  * SplitMix64 stream (tag, first_instance + k); bench inputs never cross PCIe. */

@@ -93,3 +93,61 @@ def deserialize(msg: bytes):
     digests = [msg[p + 32 * j: p + 32 * j + 32] for j in range(k)]
     root = msg[p + 32 * k: p + 32 * k + 32]
     return OK, tag, merkle.Proof(msg[12:12 + vlen], index, digests, root)
+
+
+# ----------------------------------------------------------------------------- signed frames
+# hydrabadger's own framing (in the reference: src/lib.rs:352-447):
+# WireMessages::start_send = bincode(SignedWireMessage { message, sig }) in a
+# tokio LengthDelimitedCodec frame (default: 4-byte big-endian length);
+# WireMessages::poll verifies the signature only for WireMessageKind::Message
+# (variant 7) and ::KeyGen (9) of the 11 variants at src/lib.rs:250-270.
+# Signature serialises as its 96-byte compressed G2 point, a serde tuple
+# (threshold_crypto serde_impl::projective) — no length; parity unpinned.
+KIND_MESSAGE, KIND_KEYGEN, KIND_MAX = 7, 9, 10
+E_WIRE_FRAME = -32
+E_INVALID_SIGNATURE = -33
+E_UNKNOWN_PEER = -34
+E_INVALID_POINT = -22
+
+
+def frame_len(msg_len: int) -> int:
+    return 4 + 8 + msg_len + 96
+
+
+def signed_frame(message: bytes, sig96: bytes) -> bytes:
+    """One codec frame of SignedWireMessage { message, sig }."""
+    body = struct.pack("<Q", len(message)) + bytes(message) + bytes(sig96)
+    return struct.pack(">I", len(body)) + body
+
+
+def poll_frame(frame: bytes, peer_pk=None) -> int:
+    """WireMessages::poll outcome for one received frame: 0 or an E_* code.
+    peer_pk: G1 point (oracle form) or None (unknown peer)."""
+    from . import bls12_381 as B
+    from . import tcrypto as T
+    frame = bytes(frame)
+    if len(frame) < 4:
+        return E_WIRE_EOF
+    if struct.unpack_from(">I", frame, 0)[0] != len(frame) - 4:
+        return E_WIRE_FRAME
+    if len(frame) < 12:
+        return E_WIRE_EOF
+    (mlen,) = struct.unpack_from("<Q", frame, 4)
+    if mlen > len(frame) - 12 or len(frame) - 12 - mlen < 96:
+        return E_WIRE_EOF
+    message = frame[12:12 + mlen]
+    try:
+        sig = B.g2_decompress(frame[12 + mlen:12 + mlen + 96])
+    except ValueError:
+        return E_INVALID_POINT
+    if mlen < 4:
+        return E_WIRE_EOF
+    (kind,) = struct.unpack_from("<I", message, 0)
+    if kind > KIND_MAX:
+        return E_WIRE_TAG
+    if kind in (KIND_MESSAGE, KIND_KEYGEN):
+        if peer_pk is None:
+            return E_UNKNOWN_PEER
+        if not T.verify(peer_pk, sig, message):
+            return E_INVALID_SIGNATURE
+    return OK
