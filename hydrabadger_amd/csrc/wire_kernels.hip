@@ -68,22 +68,27 @@ __device__ inline uint8_t proof_msg_byte(uint64_t o, uint32_t tag, uint64_t L, c
     return lev[(uint64_t)(nodes - 1) * 32 + (d - 32ull * k)];
 }
 
-// 16 bytes starting at an arbitrary byte address p, from 4/5 aligned dwords.
-// Every dword read contains at least one byte of [p, p + 16).
+// 16 bytes starting at an arbitrary byte address p: one dwordx4 load at the
+// dword-aligned address below p (+ one dword when p is not dword aligned) and
+// 4 v_alignbyte.  Every dword read contains at least one byte of [p, p + 16).
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* p) {
     const uint32_t s = (uint32_t)((uintptr_t)p & 3u);
     const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
-    uint32_t v[5];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = w[j];
-    v[4] = s ? w[4] : 0u;
+    const u32x4_a4 v = *reinterpret_cast<const u32x4_a4*>(w);
+    const uint32_t v4 = s ? w[4] : 0u;
     uint4 r;
-    r.x = __builtin_amdgcn_alignbyte(v[1], v[0], s);
-    r.y = __builtin_amdgcn_alignbyte(v[2], v[1], s);
-    r.z = __builtin_amdgcn_alignbyte(v[3], v[2], s);
-    r.w = __builtin_amdgcn_alignbyte(v[4], v[3], s);
+    r.x = __builtin_amdgcn_alignbyte(v.y, v.x, s);
+    r.y = __builtin_amdgcn_alignbyte(v.z, v.y, s);
+    r.z = __builtin_amdgcn_alignbyte(v.w, v.z, s);
+    r.w = __builtin_amdgcn_alignbyte(v4, v.w, s);
     return r;
 }
+
+// Every thread of the byte movers below owns kChunks 16-B chunks, 256 apart
+// (coalesced per pass); a block covers kChunks * 4 KiB of one message.
+constexpr uint32_t kChunks = 4;
+constexpr uint32_t kBlockBytes = 256 * 16 * kChunks;
 
 // grid: m messages x blocks_per_msg; thread = one 16-B destination chunk.
 __global__ __launch_bounds__(256) void rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* __restrict__ shards,
@@ -101,20 +106,22 @@ __global__ __launch_bounds__(256) void rbc_write_proof_msgs(uint32_t N, uint64_t
     const uint32_t k = proof_digests(N, i);
     const uint64_t start = out_off[j], end = out_off[j + 1];
     if (end - start != 12 + L + 16 + 32ull * k + 32) return;  // layout mismatch: host mode rejects it up front
-    const uint64_t c = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 + threadIdx.x;
-    const uint64_t A = (start & ~15ull) + 16 * c;  // byte offset in out of this chunk
-    if (A >= end) return;
     const uint64_t ki = inst[j];
     if (ki >= n) return;
     const uint8_t* row = shards + (ki * N + i) * S;
     const uint8_t* lev = levels + ki * nodes * 32ull;
-    if (A >= start + 12 && A + 16 <= start + 12 + L) {  // interior of the value: 16-B move
-        const uint64_t s = A - start - 12;
-        *reinterpret_cast<uint4*>(out + A) = load16_unaligned(row + s);
-        return;
+    const uint64_t c0 = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 * kChunks + threadIdx.x;
+#pragma unroll
+    for (uint32_t q = 0; q < kChunks; ++q) {
+        const uint64_t A = (start & ~15ull) + 16 * (c0 + 256 * q);  // byte offset in out of this chunk
+        if (A >= end) return;
+        if (A >= start + 12 && A + 16 <= start + 12 + L) {  // interior of the value: 16-B move
+            *reinterpret_cast<uint4*>(out + A) = load16_unaligned(row + (A - start - 12));
+            continue;
+        }
+        const uint64_t lo = A > start ? A : start, hi = A + 16 < end ? A + 16 : end;
+        for (uint64_t b = lo; b < hi; ++b) out[b] = proof_msg_byte(b - start, tag, L, row, lev, nodes, N, i, k);
     }
-    const uint64_t lo = A > start ? A : start, hi = A + 16 < end ? A + 16 : end;
-    for (uint64_t b = lo; b < hi; ++b) out[b] = proof_msg_byte(b - start, tag, L, row, lev, nodes, N, i, k);
 }
 
 __device__ __forceinline__ uint64_t rd_le(const uint8_t* p, int nb) {
@@ -180,9 +187,12 @@ __global__ __launch_bounds__(256) void rbc_read_msgs(uint64_t L, const uint8_t* 
     if (j >= m) return;
     const uint64_t start = msg_off[j], len = msg_off[j + 1] - start;
     const uint8_t* msg = msgs + start;
-    const MsgHdr h = parse_hdr(msg, len, L);
-    const uint64_t c = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 + threadIdx.x;
-    if (c == 0) {
+    __shared__ MsgHdr sh;  // parsed once per block (byte loads of a uniform header)
+    if (threadIdx.x == 0) sh = parse_hdr(msg, len, L);
+    __syncthreads();
+    const MsgHdr h = sh;
+    const uint64_t c0 = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 * kChunks + threadIdx.x;
+    if (c0 == 0) {
         status[j] = h.status;
         tag_out[j] = h.tag;
         const bool proof = h.tag <= HBG_MSG_ECHO && (h.status == 0 || h.status == HBG_E_INCORRECT_SHARD_SIZE);
@@ -204,15 +214,18 @@ __global__ __launch_bounds__(256) void rbc_read_msgs(uint64_t L, const uint8_t* 
         }
     }
     if (h.status != 0 || h.tag > HBG_MSG_ECHO) return;
-    const uint64_t o = 16 * c;  // value byte offset of this chunk
-    if (o >= L) return;
-    uint8_t* dst = values + j * vstride + o;
-    const uint8_t* src = msg + 12 + o;
-    if (o + 16 <= L) {
-        *reinterpret_cast<uint4*>(dst) = load16_unaligned(src);
-        return;
+#pragma unroll
+    for (uint32_t q = 0; q < kChunks; ++q) {
+        const uint64_t o = 16 * (c0 + 256 * q);  // value byte offset of this chunk
+        if (o >= L) return;
+        uint8_t* dst = values + j * vstride + o;
+        const uint8_t* src = msg + 12 + o;
+        if (o + 16 <= L) {
+            *reinterpret_cast<uint4*>(dst) = load16_unaligned(src);
+            continue;
+        }
+        for (uint64_t b = 0; o + b < L; ++b) dst[b] = src[b];
     }
-    for (uint64_t b = 0; o + b < L; ++b) dst[b] = src[b];
 }
 
 // WireMessages::start_send framing: u32 BE (8 + len + 96) | u64 LE len |
@@ -228,32 +241,35 @@ __global__ __launch_bounds__(256) void wire_frame_pack(uint64_t n, const uint8_t
     const uint64_t len = msg_off[k + 1] - msg_off[k];
     const uint64_t start = frame_off[k], end = frame_off[k + 1];
     if (end - start != 12 + len + 96) return;
-    const uint64_t c = (uint64_t)(blockIdx.x % blocks_per_frame) * 256 + threadIdx.x;
-    const uint64_t A = (start & ~15ull) + 16 * c;
-    if (A >= end) return;
     const uint8_t* m = msg + msg_off[k];
-    if (A >= start + 12 && A + 16 <= start + 12 + len) {
-        *reinterpret_cast<uint4*>(frames + A) = load16_unaligned(m + (A - start - 12));
-        return;
-    }
-    const uint64_t lo = A > start ? A : start, hi = A + 16 < end ? A + 16 : end;
     const uint64_t body = 8 + len + 96;
-    for (uint64_t b = lo; b < hi; ++b) {
-        const uint64_t o = b - start;
-        uint8_t v;
-        if (o < 4) v = (uint8_t)(body >> (8 * (3 - o)));
-        else if (o < 12) v = le_byte(len, (uint32_t)(o - 4));
-        else if (o < 12 + len) v = m[o - 12];
-        else v = sig96[96 * k + (o - 12 - len)];
-        frames[b] = v;
+    const uint64_t c0 = (uint64_t)(blockIdx.x % blocks_per_frame) * 256 * kChunks + threadIdx.x;
+#pragma unroll
+    for (uint32_t q = 0; q < kChunks; ++q) {
+        const uint64_t A = (start & ~15ull) + 16 * (c0 + 256 * q);
+        if (A >= end) return;
+        if (A >= start + 12 && A + 16 <= start + 12 + len) {
+            *reinterpret_cast<uint4*>(frames + A) = load16_unaligned(m + (A - start - 12));
+            continue;
+        }
+        const uint64_t lo = A > start ? A : start, hi = A + 16 < end ? A + 16 : end;
+        for (uint64_t b = lo; b < hi; ++b) {
+            const uint64_t o = b - start;
+            uint8_t v;
+            if (o < 4) v = (uint8_t)(body >> (8 * (3 - o)));
+            else if (o < 12) v = le_byte(len, (uint32_t)(o - 4));
+            else if (o < 12 + len) v = m[o - 12];
+            else v = sig96[96 * k + (o - 12 - len)];
+            frames[b] = v;
+        }
     }
 }
 
 hipError_t launch_wire_frame_pack(uint64_t n, const uint8_t* msg, const uint64_t* msg_off, const uint8_t* sig96,
                                   uint8_t* frames, const uint64_t* frame_off, uint64_t max_len, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    const uint64_t chunks = (12 + max_len + 96) / 16 + 2;
-    const uint32_t bpf = (uint32_t)((chunks + 255) / 256);
+    const uint64_t bpf64 = ((12 + max_len + 96) + 32 + kBlockBytes - 1) / kBlockBytes;
+    const uint32_t bpf = (uint32_t)bpf64;
     hipLaunchKernelGGL(wire_frame_pack, dim3((uint32_t)(n * bpf)), dim3(256), 0, st, n, msg, msg_off, sig96, frames,
                        frame_off, bpf);
     return hipGetLastError();
@@ -265,8 +281,7 @@ hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* sh
                                        const uint64_t* out_off, hipStream_t st) {
     if (m == 0) return hipSuccess;
     const uint64_t max_len = 12 + L + 16 + 32ull * merkle_depth(N) + 32;
-    const uint64_t chunks = max_len / 16 + 2;
-    const uint32_t bpm = (uint32_t)((chunks + 255) / 256);
+    const uint32_t bpm = (uint32_t)((max_len + 32 + kBlockBytes - 1) / kBlockBytes);
     hipLaunchKernelGGL(rbc_write_proof_msgs, dim3((uint32_t)(m * bpm)), dim3(256), 0, st, N, L, shards, S, levels,
                        merkle_nodes(N), n, tag, m, inst, index, out, out_off, bpm);
     return hipGetLastError();
@@ -277,7 +292,7 @@ hipError_t launch_rbc_read_msgs(uint32_t N, uint64_t L, const uint8_t* msgs, con
                                 uint8_t* digests, uint32_t* ndig, uint8_t* roots, int32_t* status,
                                 hipStream_t st) {
     if (m == 0) return hipSuccess;
-    const uint32_t bpm = (uint32_t)(((L + 15) / 16 + 255) / 256 + (L == 0 ? 1 : 0));
+    const uint32_t bpm = (uint32_t)((L + kBlockBytes - 1) / kBlockBytes + (L == 0 ? 1 : 0));
     hipLaunchKernelGGL(rbc_read_msgs, dim3((uint32_t)(m * (bpm ? bpm : 1))), dim3(256), 0, st, L, msgs, msg_off,
                        m, tag, values, vstride, index, digests, merkle_depth(N), ndig, roots, status,
                        bpm ? bpm : 1u);
