@@ -870,14 +870,73 @@ TDEC_KERNEL void tdec_combine(uint32_t n, uint32_t t, const uint8_t* __restrict_
     for (uint64_t i = 0; i < len; ++i) out[off + i] = V[off + i] ^ (uint8_t)(rng.next_u32() & 0xFFu);
 }
 
-// [l]P for a 255-bit canonical scalar (8 LE words), P affine: double-and-add.
+// GLV split on G1 (Gallant–Lambert–Vanstone): phi(x, y) = (beta x, y) acts as
+// [-x^2] on G1 (the subgroup check above), so for l = q x^2 + rem
+// [l]P = [rem]P + [q]([x^2]P) with [x^2]P = (beta px, -py); rem < x^2 < 2^128
+// and q < 2^129 for any 256-bit l.  x^2 = 0xac45a4010001a402_00000001_00000000.
+inline constexpr uint32_t kX2[4] = {0x00000000u, 0x00000001u, 0x0001a402u, 0xac45a401u};
+
+BD void split_x2(const uint32_t (&l)[8], uint32_t (&q)[5], uint32_t (&rm)[5]) {
+#pragma unroll
+    for (int w = 0; w < 5; ++w) q[w] = rm[w] = 0u;
+#pragma unroll
+    for (int w = 7; w >= 0; --w) {  // schoolbook binary long division, static word indices
+        const uint32_t lw = l[w];
+        uint32_t qw = 0;
+#pragma unroll 1
+        for (int b = 31; b >= 0; --b) {
+#pragma unroll
+            for (int i = 4; i > 0; --i) rm[i] = (rm[i] << 1) | (rm[i - 1] >> 31);
+            rm[0] = (rm[0] << 1) | ((lw >> b) & 1u);
+            bool ge = rm[4] != 0, decided = ge;
+#pragma unroll
+            for (int i = 3; i >= 0; --i)
+                if (!decided && rm[i] != kX2[i]) {
+                    ge = rm[i] > kX2[i];
+                    decided = true;
+                }
+            if (!decided) ge = true;  // equal
+            if (ge) {
+                uint32_t borrow = 0;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    const uint64_t d = (uint64_t)rm[i] - (i < 4 ? kX2[i] : 0u) - borrow;
+                    rm[i] = (uint32_t)d;
+                    borrow = (uint32_t)(d >> 63);
+                }
+                qw |= 1u << b;
+            }
+        }
+        if (w < 5) q[w] = qw;  // q < 2^129: words 5..7 of the quotient are zero
+    }
+}
+
+// [l]P for a 256-bit scalar (8 LE words, any value: [l]P = [l mod r]P), P
+// affine and in G1: joint double-and-add (Straus–Shamir) over the 129-bit GLV
+// halves with the three points P, [x^2]P and their sum.  Branch-free per step
+// (one Jacobian add whose operand is selected per lane) so lanes with
+// different scalars stay converged: 129 doublings + 129 adds instead of 256
+// doublings + 256 (divergent) mixed adds.
 BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
-    G1 r = {fp_one(), fp_one(), fp_zero()};
-    int top = 254;
-    while (top >= 0 && !((l[top >> 5] >> (top & 31)) & 1u)) --top;
-    for (int bit = top; bit >= 0; --bit) {
-        r = g1_dbl(r);
-        if ((l[bit >> 5] >> (bit & 31)) & 1u) r = g1_add_mixed(r, px, py);
+    uint32_t q[5], rm[5];
+    split_x2(l, q, rm);
+    const Fp bx = fp_mul(px, fp_const(kBeta)), by = fp_neg(py);  // [x^2]P
+    const G1 both = g1_add_mixed({px, py, fp_one()}, bx, by);    // P + [x^2]P (never infinity)
+    G1 r = {fp_one(), fp_one(), fp_zero()};  // doubling / adding to infinity stays exact
+#pragma unroll
+    for (int w = 4; w >= 0; --w) {
+        const uint32_t qw = q[w], rw = rm[w];
+#pragma unroll 1
+        for (int bit = (w == 4 ? 0 : 31); bit >= 0; --bit) {
+            r = g1_dbl(r);
+            const bool a = (rw >> bit) & 1u, b = (qw >> bit) & 1u;
+            G1 t;
+            t.x = a ? (b ? both.x : px) : bx;
+            t.y = a ? (b ? both.y : py) : by;
+            t.z = (a && b) ? both.z : fp_one();
+            const G1 sum = g1_add(r, t);
+            if (a || b) r = sum;
+        }
     }
     return r;
 }
