@@ -1027,13 +1027,32 @@ BD void load_scalar(const uint8_t* p, uint32_t (&k)[8]) {
                (uint32_t)p[4 * w + 3] << 24;
 }
 
+// [k]P for P in G2 (affine) and a 256-bit scalar: psi acts as [x] on G2, so
+// psi^2 = [x^2] and the G1 split applies unchanged — k = q x^2 + rem,
+// [k]P = [rem]P + [q]psi^2(P) (psi^2 of an affine point is affine) — with the
+// same branch-free joint double-and-add: 129 doublings + 129 additions instead
+// of 256 + 256 divergent mixed additions.  Callers pass subgroup points only
+// (hash_g2 outputs; shares the crate deserialised, i.e. subgroup-checked).
 BD G2 g2_mul_scalar(const Fp2& px, const Fp2& py, const uint32_t (&k)[8]) {
+    uint32_t q[5], rm[5];
+    split_x2(k, q, rm);
+    const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));  // [x^2]P, Z = 1
+    const G2 both = g2_add_mixed({px, py, fp2_one()}, B.x, B.y);
     G2 r = {fp2_one(), fp2_one(), fp2_zero()};
-    int top = 255;
-    while (top >= 0 && !((k[top >> 5] >> (top & 31)) & 1u)) --top;
-    for (int bit = top; bit >= 0; --bit) {
-        r = g2_dbl(r);
-        if ((k[bit >> 5] >> (bit & 31)) & 1u) r = g2_add_mixed(r, px, py);
+#pragma unroll
+    for (int w = 4; w >= 0; --w) {
+        const uint32_t qw = q[w], rw = rm[w];
+#pragma unroll 1
+        for (int bit = (w == 4 ? 0 : 31); bit >= 0; --bit) {
+            r = g2_dbl(r);
+            const bool a = (rw >> bit) & 1u, b = (qw >> bit) & 1u;
+            G2 t;
+            t.x = a ? (b ? both.x : px) : B.x;
+            t.y = a ? (b ? both.y : py) : B.y;
+            t.z = (a && b) ? both.z : fp2_one();
+            const G2 sum = g2_add(r, t);
+            if (a || b) r = sum;
+        }
     }
     return r;
 }
