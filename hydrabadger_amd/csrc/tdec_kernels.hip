@@ -540,6 +540,7 @@ TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_af
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // (pk, w, v)
     if (i >= n_pk * 2048u) return;
     const uint32_t pk = i >> 11, w = (i >> 8) & 7u, v = i & 255u;
+    if (w >= 4) return;  // batch weights use 32-bit halves: windows 0..3
     const uint32_t* pa = pk_aff + 32ull * pk;
     uint32_t* o = tbl + (uint64_t)pk * kPkTblWords + (uint64_t)(w * 256 + v) * 24;
     if (v == 0 || pa[24] != 0) return;
@@ -552,6 +553,28 @@ TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_af
 // weight, and the quad / 16-group / batch sums by cross-lane butterfly
 // (ds_swizzle/bpermute shuffles: no LDS for the points, so occupancy is set
 // by VGPRs alone).
+// [a]P + [b]([x^2]P) for P in G1 (affine) and 32-bit a, b: on G1 [x^2]P =
+// -phi(P) = (beta px, -py), so the batch weight r = a + b x^2 (mod r; the
+// 2^64 pairs give 2^64 distinct weights) costs a 32-bit joint double-and-add
+// (branch-free addend select, as g1_mul_fr) instead of a 64-bit one.
+BD G1 g1_mul_ab32(const Fp& px, const Fp& py, uint32_t a, uint32_t b) {
+    const Fp bx = fp_mul(px, fp_const(kBeta)), by = fp_neg(py);
+    const G1 both = g1_add_mixed({px, py, fp_one()}, bx, by);  // P + [x^2]P (never infinity)
+    G1 r = {fp_one(), fp_one(), fp_zero()};
+#pragma unroll 1
+    for (int bit = 31; bit >= 0; --bit) {
+        r = g1_dbl(r);
+        const bool ea = (a >> bit) & 1u, eb = (b >> bit) & 1u;
+        G1 t;
+        t.x = ea ? (eb ? both.x : px) : bx;
+        t.y = ea ? (eb ? both.y : py) : by;
+        t.z = (ea && eb) ? both.z : fp_one();
+        const G1 sum = g1_add(r, t);
+        if (ea || eb) r = sum;
+    }
+    return r;
+}
+
 TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
                                                         const uint32_t* __restrict__ perm,
                                                         const uint8_t* __restrict__ share48,
@@ -592,23 +615,32 @@ TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
         for (int i = 0; i < 32; ++i) m[i] = sBatch[i];
         for (int i = 0; i < 4; ++i) m[32 + i] = (uint8_t)(lane >> (8 * i));
         sha3_bytes(m, 36, dg);
-        uint64_t r = 0;
-        for (int i = 0; i < 8; ++i) r |= (uint64_t)dg[i] << (8 * i);
-        r |= 1ull;  // nonzero
-        if (!s.inf) A = g1_mul_u64(s.x, s.y, r);
+        // weight r_i = a + b x^2 (a odd: nonzero); S_i and pk_i are in G1
+        // (decoded with the subgroup check), where [x^2]P = (beta px, -py)
+        uint32_t ra = 0, rb = 0;
+        for (int i = 0; i < 4; ++i) {
+            ra |= (uint32_t)dg[i] << (8 * i);
+            rb |= (uint32_t)dg[4 + i] << (8 * i);
+        }
+        ra |= 1u;
+        if (!s.inf) A = g1_mul_ab32(s.x, s.y, ra, rb);
         const uint32_t* pa = pk_aff + 32ull * pk;
         if (pa[24] == 0) {
-            if (pk_tbl) {
+            if (pk_tbl) {  // windows 0..3 of the [v 256^w]pk table; the b half through (beta x, -y)
                 const uint32_t* t = pk_tbl + (uint64_t)pk * kPkTblWords;
-                for (int w = 0; w < 8; ++w) {
-                    const uint32_t v = (uint32_t)(r >> (8 * w)) & 255u;
-                    if (v) {
-                        const uint32_t* e = t + (w * 256 + v) * 24;
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t va = (ra >> (8 * w)) & 255u, vb = (rb >> (8 * w)) & 255u;
+                    if (va) {
+                        const uint32_t* e = t + (w * 256 + va) * 24;
                         B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+                    }
+                    if (vb) {
+                        const uint32_t* e = t + (w * 256 + vb) * 24;
+                        B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
                     }
                 }
             } else {
-                B = g1_mul_u64(load_fp(pa), load_fp(pa + 12), r);
+                B = g1_mul_ab32(load_fp(pa), load_fp(pa + 12), ra, rb);
             }
         }
     }
@@ -1338,6 +1370,27 @@ TDEC_KERNEL void sig_doc_prepare(uint32_t n, const uint8_t* __restrict__ doc, co
 // (D = SHA3 of the leaf digests SHA3(doc seed || share || key index)), then
 // [r_i] sig_i (G2) and [r_i] pk_i (G1, fixed-base tables when given) and the
 // quad / 16-group / batch sums by cross-lane butterflies.
+// [a]P + [b]psi^2(P) = [a + b x^2]P for P in G2 (affine), 32-bit a, b (psi = [x]
+// on G2; psi^2 of an affine point is affine) — the G2 half of the coin
+// shares' batch weights, same joint double-and-add as g1_mul_ab32.
+BD G2 g2_mul_ab32(const Fp2& px, const Fp2& py, uint32_t a, uint32_t b) {
+    const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));
+    const G2 both = g2_add_mixed({px, py, fp2_one()}, B.x, B.y);
+    G2 r = {fp2_one(), fp2_one(), fp2_zero()};
+#pragma unroll 1
+    for (int bit = 31; bit >= 0; --bit) {
+        r = g2_dbl(r);
+        const bool ea = (a >> bit) & 1u, eb = (b >> bit) & 1u;
+        G2 t;
+        t.x = ea ? (eb ? both.x : px) : B.x;
+        t.y = ea ? (eb ? both.y : py) : B.y;
+        t.z = (ea && eb) ? both.z : fp2_one();
+        const G2 sum = g2_add(r, t);
+        if (ea || eb) r = sum;
+    }
+    return r;
+}
+
 TDEC_KERNEL void sig_batch_leaves(const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                   const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_pk,
                                   const uint8_t* __restrict__ seeds, const uint32_t* __restrict__ pk_aff,
@@ -1363,14 +1416,17 @@ TDEC_KERNEL void sig_batch_leaves(const BatchDesc* __restrict__ desc, const uint
     __syncthreads();
     if (lane == 0) sha3_bytes(sDig, 32u * (d.end - d.start), sBatch);
     __syncthreads();
-    uint64_t r = 0;
+    uint32_t ra = 0, rb = 0;  // weight r_i = a + b x^2 (a odd: nonzero); pk_i in G1, sig_i in G2
     if (valid) {
         uint8_t m[36], dg[32];
         for (int i = 0; i < 32; ++i) m[i] = sBatch[i];
         for (int i = 0; i < 4; ++i) m[32 + i] = (uint8_t)(lane >> (8 * i));
         sha3_bytes(m, 36, dg);
-        for (int i = 0; i < 8; ++i) r |= (uint64_t)dg[i] << (8 * i);
-        r |= 1ull;  // nonzero
+        for (int i = 0; i < 4; ++i) {
+            ra |= (uint32_t)dg[i] << (8 * i);
+            rb |= (uint32_t)dg[4 + i] << (8 * i);
+        }
+        ra |= 1u;
     }
     leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
     uint32_t* out = sums + (uint64_t)b * kSigBatchSumWords;
@@ -1379,17 +1435,21 @@ TDEC_KERNEL void sig_batch_leaves(const BatchDesc* __restrict__ desc, const uint
         G1 B = {fp_one(), fp_one(), fp_zero()};
         const uint32_t* pa = pk_aff + 32ull * pk;
         if (valid && pa[24] == 0) {
-            if (pk_tbl) {
+            if (pk_tbl) {  // windows 0..3 of the [v 256^w]pk table; the b half through (beta x, -y)
                 const uint32_t* t = pk_tbl + (uint64_t)pk * kPkTblWords;
-                for (int w = 0; w < 8; ++w) {
-                    const uint32_t v = (uint32_t)(r >> (8 * w)) & 255u;
-                    if (v) {
-                        const uint32_t* e = t + (w * 256 + v) * 24;
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t va = (ra >> (8 * w)) & 255u, vb = (rb >> (8 * w)) & 255u;
+                    if (va) {
+                        const uint32_t* e = t + (w * 256 + va) * 24;
                         B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+                    }
+                    if (vb) {
+                        const uint32_t* e = t + (w * 256 + vb) * 24;
+                        B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
                     }
                 }
             } else {
-                B = g1_mul_u64(load_fp(pa), load_fp(pa + 12), r);
+                B = g1_mul_ab32(load_fp(pa), load_fp(pa + 12), ra, rb);
             }
         }
 #pragma unroll 1
@@ -1403,7 +1463,7 @@ TDEC_KERNEL void sig_batch_leaves(const BatchDesc* __restrict__ desc, const uint
     // G2 side: sum r_i sig_i
     {
         G2 A = {fp2_one(), fp2_one(), fp2_zero()};
-        if (valid && !s.inf) A = g2_mul_u64(s.x, s.y, r);
+        if (valid && !s.inf) A = g2_mul_ab32(s.x, s.y, ra, rb);
 #pragma unroll 1
         for (int m = 1; m < 64; m <<= 1) {
             A = g2_add(A, g2_shfl_xor(A, m));
