@@ -143,12 +143,41 @@ BD bool fp_raw_lt_p(const Fp& a) {
     return br != 0;
 }
 
-// a^e for an exponent held in constant memory (nbits significant bits).
+// a^e for an exponent held in constant memory (nbits significant bits, top
+// bit set).  Sliding window of 4 bits over the odd powers a, a^3, .., a^15:
+// the exponent is wave-uniform, so every branch below is uniform; 8 table
+// multiplications + ~nbits/5 window multiplications instead of ~nbits/2
+// (Fermat inverse: 380 squarings + 83 multiplications instead of + 190).
 __device__ __noinline__ Fp fp_pow(Fp a, const uint32_t* __restrict__ e, int nbits) {
-    Fp r = a;
-    for (int i = nbits - 2; i >= 0; --i) {
-        r = fp_sqr(r);
-        if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+    Fp tbl[8];
+    tbl[0] = a;
+    const Fp a2 = fp_sqr(a);
+#pragma unroll 1
+    for (int k = 1; k < 8; ++k) tbl[k] = fp_mul(tbl[k - 1], a2);
+    auto bit = [&](int i) -> uint32_t { return (e[i >> 5] >> (i & 31)) & 1u; };
+    Fp r = fp_one();  // squarings of one before the first window (a leading zero bit) stay one
+    bool first = true;
+    int i = nbits - 1;
+#pragma unroll 1
+    while (i >= 0) {
+        if (!bit(i)) {
+            r = fp_sqr(r);
+            --i;
+            continue;
+        }
+        int j = i - 3 > 0 ? i - 3 : 0;  // window [j, i] ending in a set bit
+        while (!bit(j)) ++j;
+        uint32_t v = 0;
+        for (int k = i; k >= j; --k) v = (v << 1) | bit(k);
+        if (first) {
+            r = tbl[v >> 1];
+            first = false;
+        } else {
+#pragma unroll 1
+            for (int k = i; k >= j; --k) r = fp_sqr(r);
+            r = fp_mul(r, tbl[v >> 1]);
+        }
+        i = j - 1;
     }
     return r;
 }
