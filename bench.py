@@ -83,6 +83,22 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(instances: int) -> dict:
+    """HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, separate runs: tools/pmc.sh) at this launch shape, from
+    profiles/pmc_traffic.json; empty when the shape differs."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    out = {"source": d.get("source", "") + f" ({os.path.relpath(path, ROOT)})"}
+    for k in ("merkle_build", "rs_encode_const_22_42"):
+        if d.get(k, {}).get("instances") == instances:
+            out[k] = d[k]["hbm_bytes_per_launch"]
+    return out
+
+
 def timed(fn, reps: int):
     """Average ms per call of fn over reps (events on the current stream)."""
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -556,19 +572,22 @@ def main():
     ms_step = timed(step, reps)
     ms_encode = max(ms_step - ms_merkle, 0.0)
     ops, mbytes = merkle_alg(N_NODES, L)
+    traffic = pmc_traffic(B)
     achieved_ops = ops * B / (ms_merkle * 1e-3)
     enc_bytes = B * (PAYLOAD + N_NODES * L)  # read payload, write N shards
     roofline = {
         "kernel": "merkle_build (SHA3-256 leaves + pair tree)",
         "bound": "valu", "unit": "Tops/s",
         "achieved": achieved_ops / 1e12, "peak": VALU_PEAK / 1e12, "frac": achieved_ops / VALU_PEAK,
-        "traffic": None,
+        "traffic": traffic.get("merkle_build"), "traffic_unit": "HBM bytes per launch (PMC)",
+        "traffic_source": traffic.get("source"),
         "alg_ops_per_instance": ops, "keccak_f_ops": KECCAK_F_OPS,
         "hbm": {"achieved_GBps": mbytes * B / (ms_merkle * 1e-3) / 1e9, "peak_GBps": HBM_PEAK / 1e9,
                 "frac": mbytes * B / (ms_merkle * 1e-3) / HBM_PEAK, "alg_bytes_per_instance": mbytes},
         "avg_ms": ms_merkle, "instances_per_launch": B,
     }
     kernels = {"merkle_build_ms": ms_merkle, "rs_encode_const_22_42_ms": ms_encode,
+               "rs_encode_traffic_bytes_per_launch": traffic.get("rs_encode_const_22_42"),
                "rs_encode_hbm_GBps": enc_bytes / (ms_encode * 1e-3) / 1e9 if ms_encode > 0 else None}
 
     # ---- decode path: reconstruct exactly 2f erasures + tree + glue ----
