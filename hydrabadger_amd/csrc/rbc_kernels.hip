@@ -60,7 +60,10 @@ __device__ __forceinline__ void mac_column(uint32_t (&acc)[Q], const NibPair& T,
 // (J*L mod 4) is uniform: one dwordx2 load + v_alignbyte per word, no
 // per-lane branches.  Loads run kPrefetch columns ahead of the arithmetic.
 typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
-constexpr int kPrefetch = 6;
+#ifndef HBG_ENC_PREFETCH
+#define HBG_ENC_PREFETCH 6
+#endif
+constexpr int kPrefetch = HBG_ENC_PREFETCH;
 
 template <int D, int Q, int MODE>
 struct EncodeCtx {
