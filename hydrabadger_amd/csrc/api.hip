@@ -46,6 +46,7 @@ struct hbg_ctx {
     // (pk fixed-base tables when each key verifies >= kPkTableMinUses shares), 2 batched + tables always
     // (and, for signature shares, no speculative 16-group round)
     int tdec_batched = 1;
+    int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
     std::mutex mu;
 };
 
@@ -158,10 +159,22 @@ int device_encode_plan(hbg_ctx* c, uint32_t D, uint32_t Q, uint8_t** out) {
 
 bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p % a) == 0; }
 
+// Synchronise the context stream and return (and clear) the first error a
+// kernel flagged since the last such point (dev_err.h).
+int sync_status(hbg_ctx* c) {
+    int32_t e = 0;
+    HBG_TRY(hipMemcpyAsync(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
+    HBG_TRY(hipStreamSynchronize(c->stream));
+    if (e != 0) HBG_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
+    return e;
+}
+
+// End of a call: HBG_DEVICE | HBG_ASYNC returns right after enqueueing (no
+// host synchronisation anywhere in such a call, apart from growing a scratch
+// slot); otherwise synchronise and report device-side argument errors.
 int finish(hbg_ctx* c, uint32_t flags) {
     if ((flags & HBG_DEVICE) && (flags & HBG_ASYNC)) return HBG_OK;
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 // Encode parity for n instances on a device buffer with row stride S.
@@ -254,7 +267,11 @@ int hbg_init(hbg_ctx** out, int device) {
         return HBG_E_DEVICE;
     }
     c->stream = c->own;
-    if (const char* e = getenv("HBG_TDEC_BATCHED")) c->tdec_batched = atoi(e);
+    if (hipMalloc(&c->d_err, sizeof(int32_t)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int32_t)) != hipSuccess) {
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return HBG_E_DEVICE;
+    }
     *out = c;
     return HBG_OK;
 }
@@ -267,6 +284,7 @@ void hbg_free(hbg_ctx* c) {
         if (b.p) (void)hipFree(b.p);
     for (auto& kv : c->matrices) (void)hipFree(kv.second);
     for (auto& kv : c->enc_plans) (void)hipFree(kv.second);
+    (void)hipFree(c->d_err);
     (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -287,8 +305,9 @@ int hbg_reset_stream(hbg_ctx* c) {
 
 int hbg_sync(hbg_ctx* c) {
     if (!c) return HBG_E_ARG;
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    return sync_status(c);
 }
 
 int hbg_rs_encode(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t stride, uint64_t n,
@@ -312,8 +331,7 @@ int hbg_rs_encode(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shard
     HBG_TRY(hipMemcpy2DAsync(d, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
     HBG_CHECK(encode_device(c, D, Q, L, (uint8_t*)d, S, n, nullptr, 0, nullptr));
     HBG_TRY(hipMemcpy2DAsync(shards, stride, d, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 int hbg_rs_reconstruct(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t stride,
@@ -342,9 +360,9 @@ int hbg_rs_reconstruct(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* 
     HBG_TRY(hipMemcpy2DAsync(shards, stride, d, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
     std::vector<int32_t> st(n);
     HBG_TRY(hipMemcpyAsync(st.data(), ds, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
+    const int rc = sync_status(c);
     if (status) memcpy(status, st.data(), sizeof(int32_t) * n);
-    return HBG_OK;
+    return rc;
 }
 
 int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, uint64_t stride, uint8_t* levels,
@@ -366,8 +384,7 @@ int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, 
     if (L) HBG_TRY(hipMemcpy2DAsync(d, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
     HBG_TRY(launch_merkle_build((const uint8_t*)d, S, L, N, n, (uint8_t*)dl, c->stream));
     HBG_TRY(hipMemcpyAsync(levels, dl, (size_t)nodes * 32 * n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
@@ -402,8 +419,7 @@ int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* val
     HBG_TRY(launch_merkle_validate(N, len, (const uint8_t*)dv, S, (const uint32_t*)di, (const uint8_t*)dd, depth,
                                    (const uint32_t*)dn, (const uint8_t*)dr, (uint8_t*)dok, n, c->stream));
     HBG_TRY(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint64_t pstride,
@@ -418,6 +434,7 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
     const uint32_t nodes = merkle_nodes(N);
     auto run = [&](const uint8_t* dpay, uint64_t dps, const uint64_t* dplen, uint8_t* dsh, uint64_t S,
                    uint8_t* dlev) -> int {
+        HBG_TRY(launch_rbc_check_plen(n, dplen, dps, D, L, c->d_err, c->stream));
         if (Q) {
             HBG_CHECK(encode_device(c, D, Q, L, dsh, S, n, dpay, dps, dplen));
         } else {
@@ -448,8 +465,7 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
     HBG_CHECK(run((const uint8_t*)dpay, PS, (const uint64_t*)dpl, (uint8_t*)dsh, S, (uint8_t*)dl));
     HBG_TRY(hipMemcpy2DAsync(shards, stride, dsh, S, L, N * n, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpyAsync(levels, dl, (size_t)nodes * 32 * n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t stride, const uint8_t* present,
@@ -473,20 +489,7 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
             HBG_CHECK(reconstruct_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds));
         } else {
             // Trivial coding: every shard must be present (hbbft Coding::reconstruct_shards)
-            std::vector<uint8_t> h((size_t)N * n);
-            std::vector<int32_t> st(n);
-            if (flags & HBG_DEVICE) {
-                HBG_TRY(hipMemcpyAsync(h.data(), dpres, h.size(), hipMemcpyDeviceToHost, c->stream));
-                HBG_TRY(hipStreamSynchronize(c->stream));
-            } else {
-                memcpy(h.data(), present, h.size());
-            }
-            for (uint64_t k = 0; k < n; ++k) {
-                st[k] = 0;
-                for (uint32_t i = 0; i < N; ++i)
-                    if (!h[k * N + i]) st[k] = HBG_E_TOO_FEW_SHARDS_PRESENT;
-            }
-            HBG_TRY(hipMemcpyAsync(ds, st.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+            HBG_TRY(launch_rbc_trivial_status(n, N, dpres, (int32_t*)ds, c->stream));
         }
         HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream));
         HBG_TRY(launch_rbc_glue(dsh, S, L, N, D, n, (const uint8_t*)dl, droots, (const int32_t*)ds, dplen, dstat, dout,
@@ -515,8 +518,7 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
     HBG_TRY(hipMemcpyAsync(plen, dpl, 8 * n, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpy2DAsync(out, ostride, dout, OS, (uint64_t)D * L, n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 // ------------------------------------------------------------------ family 3
@@ -524,7 +526,7 @@ namespace {
 
 struct CtTable {
     uint32_t *ct_u, *coefH, *coefW;
-    int32_t* ct_status;
+    int32_t* ct_status;  // [n_ct + 1]: entry n_ct is the invalid sentinel (device-mode index check)
     const uint8_t* U48;  // device copy of the compressed U points (batch weights hash them)
 };
 
@@ -552,7 +554,7 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     }
     void *pcu, *pst, *ph, *pwc;
     HBG_CHECK(scratch(c, 4, 4ull * bls::kAffWords * n_ct, &pcu));
-    HBG_CHECK(scratch(c, 5, 4ull * n_ct, &pst));
+    HBG_CHECK(scratch(c, 5, 4ull * (n_ct + 1), &pst));
     HBG_CHECK(scratch(c, 6, 4ull * bls::kLineWordsPerPoint * n_ct, &ph));
     HBG_CHECK(scratch(c, 7, 4ull * bls::kLineWordsPerPoint * n_ct, &pwc));
     t.ct_u = (uint32_t*)pcu;
@@ -560,15 +562,26 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     t.U48 = dU;
     t.coefH = (uint32_t*)ph;
     t.coefW = (uint32_t*)pwc;
+    HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
     HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW, c->stream));
     return HBG_OK;
 }
 
+// Decode a public-key table: pk_aff [n_pk][32] and pk_status [n_pk + 1]
+// (entry n_pk: the invalid sentinel of the device-mode index check).
+int prepare_pks(hbg_ctx* c, uint32_t n_pk, const uint8_t* dpk, void** paff, void** pst) {
+    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * (n_pk ? n_pk : 1), paff));
+    HBG_CHECK(scratch(c, 13, 4ull * (n_pk + 1), pst));
+    HBG_TRY(hipMemsetAsync((int32_t*)*pst + n_pk, 0xFF, 4, c->stream));
+    if (n_pk) HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, dpk, (uint32_t*)*paff, (int32_t*)*pst, c->stream));
+    return HBG_OK;
+}
 
 // Batched PublicKeyShare::verify_decryption_share (tdec_kernels.hip, "batched
 // share verification"): sort shares by ciphertext, cut batches of <= 64,
 // weighted batch sums, then four check rounds (batch, 16-group, quad, single
-// share).  Host syncs: batch count and the item counts of rounds 1-3.
+// share).  Every round's work count is a device word read by the kernels
+// (grids sized for the bound): no host synchronisation (HBG_ASYNC contract).
 // A pk table costs ~2k G1 scalar multiplications to build and saves ~60 G1
 // doublings per share verified under that key.
 constexpr uint64_t kPkTableMinUses = 2048;
@@ -583,6 +596,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
         tbl = (uint32_t*)p;
         HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream));
     }
+    const uint32_t n_keys = n_ct + 1;  // + the sentinel ciphertext
     void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
     const size_t tb_bytes = bls::tdec_batch_temp_bytes(n);
     HBG_CHECK(scratch(c, 16, 4ull * n, &keys));
@@ -592,50 +606,47 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_CHECK(scratch(c, 20, (size_t)bls::kBatchDescBytes * n, &desc));
     HBG_CHECK(scratch(c, 21, tb_bytes, &temp));
     HBG_CHECK(scratch(c, 22, 64, &cnt));
-    uint32_t nbh[2] = {0, 0};
-    HBG_TRY(bls::launch_tdec_batch_plan(n, n_ct, dsc, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta, (uint32_t*)tb,
-                                        (bls::BatchDesc*)desc, temp, tb_bytes, nbh, c->stream));
-    const uint32_t nb = nbh[0] + nbh[1];
-    void *sums, *lok, *items, *fails;
+    const uint32_t nb = bls::tdec_batch_bound(n, n_keys);
+    void *sums, *lok, *items, *items2, *fails;
     HBG_CHECK(scratch(c, 23, (size_t)bls::kBatchSumBytes * nb, &sums));
     HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
     HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 4 * nb, &items));
-    HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
-    uint32_t* counts = (uint32_t*)cnt;  // [0] 16-group items, [1] failing shares, [2] quad items
-    void* items2;
     HBG_CHECK(scratch(c, 28, (size_t)bls::kCheckItemBytes * 16 * nb, &items2));
+    HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
+    // counts: [0] 16-group items, [1] failing shares, [2] quad items, [3] batches
+    uint32_t* counts = (uint32_t*)cnt;
+    const bls::BatchDesc* ds = (const bls::BatchDesc*)desc;
+    const uint32_t *pm = (const uint32_t*)perm, *sm = (const uint32_t*)sums;
+    const uint8_t* lk = (const uint8_t*)lok;
+    auto* it1 = (bls::CheckItem*)items;
+    auto* it2 = (bls::CheckItem*)items2;
+    HBG_TRY(hipMemsetAsync(counts, 0, 12, c->stream));
+    HBG_TRY(bls::launch_tdec_batch_plan(n, n_keys, dsc, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta,
+                                        (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, counts + 3, c->stream));
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
-    HBG_TRY(hipMemsetAsync(counts, 0, 16, c->stream));
-    HBG_TRY(bls::launch_tdec_batch_leaves(nb, (const bls::BatchDesc*)desc, (const uint32_t*)perm, dsh, dsp, dU48,
-                                          t.ct_status, paff, pst, tbl, (uint32_t*)sums, (uint8_t*)lok, c->stream));
+    HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.ct_status, paff, pst, tbl,
+                                          (uint32_t*)sums, (uint8_t*)lok, c->stream));
     // round 0: every batch sum; failing batches push their 16-share groups
-    HBG_TRY(bls::launch_tdec_batch_check(nb, nullptr, (const bls::BatchDesc*)desc, (const uint32_t*)perm,
-                                         (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u, t.coefH, t.coefW, dok,
-                                         (bls::CheckItem*)items, counts, (uint32_t*)fails, counts + 1, c->stream));
-    uint32_t h[3];
-    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
+    HBG_TRY(bls::launch_tdec_batch_check(nb, counts + 3, nullptr, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it1,
+                                         counts, (uint32_t*)fails, counts + 1, c->stream));
     // round 1: 16-share groups; failing ones push their quads
-    HBG_TRY(bls::launch_tdec_batch_check(h[0], (const bls::CheckItem*)items, (const bls::BatchDesc*)desc,
-                                         (const uint32_t*)perm, (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u,
-                                         t.coefH, t.coefW, dok, (bls::CheckItem*)items2, counts + 2,
-                                         (uint32_t*)fails, counts + 1, c->stream));
-    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
+    HBG_TRY(bls::launch_tdec_batch_check(4 * nb, counts, it1, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it2,
+                                         counts + 2, (uint32_t*)fails, counts + 1, c->stream));
     // round 2: quads; failing ones append their shares
-    HBG_TRY(bls::launch_tdec_batch_check(h[2], (const bls::CheckItem*)items2, (const bls::BatchDesc*)desc,
-                                         (const uint32_t*)perm, (const uint32_t*)sums, (const uint8_t*)lok, t.ct_u,
-                                         t.coefH, t.coefW, dok, nullptr, nullptr, (uint32_t*)fails, counts + 1,
-                                         c->stream));
-    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    if (getenv("HBG_TDEC_DEBUG"))
-        fprintf(stderr, "hbg batched verify: n=%u batches=%u 16-groups=%u quads=%u fail-shares=%u\n", n, nb, h[0],
-                h[2], h[1]);
+    HBG_TRY(bls::launch_tdec_batch_check(16 * nb, counts + 2, it2, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok,
+                                         nullptr, nullptr, (uint32_t*)fails, counts + 1, c->stream));
     // round 3: the shares of failing quads, one by one (the reference's equation)
-    HBG_TRY(bls::launch_tdec_verify_shares(h[1], dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff, pst, dok,
-                                           c->stream, (const uint32_t*)fails));
+    HBG_TRY(bls::launch_tdec_verify_shares(n, counts + 1, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff,
+                                           pst, dok, c->stream, (const uint32_t*)fails));
     return HBG_OK;
+}
+
+// Host-mode index validation (device mode: the kernels check, dev_err.h).
+bool index_ok(uint32_t flags, const uint32_t* idx, uint64_t n, uint64_t bound) {
+    if (flags & HBG_DEVICE) return true;
+    for (uint64_t k = 0; k < n; ++k)
+        if (idx[k] >= bound) return false;
+    return true;
 }
 
 }  // namespace
@@ -647,10 +658,8 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
         (n && (!share48 || !share_ct || !share_pk || !ok)))
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    if (!(flags & HBG_DEVICE)) {
-        for (uint64_t k = 0; k < n; ++k)
-            if (share_ct[k] >= n_ct || share_pk[k] >= n_pk) return HBG_E_ARG;
-    }
+    if (n_ct == 0xFFFFFFFFu || n_pk == 0xFFFFFFFFu) return HBG_E_ARG;  // the sentinels need one more index
+    if (!index_ok(flags, share_ct, n, n_ct) || !index_ok(flags, share_pk, n, n_pk)) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     CtTable t;
@@ -662,12 +671,12 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     uint8_t* dok = ok;
     if (!(flags & HBG_DEVICE)) {
         void *a, *b, *s1, *s2, *o;
-        HBG_CHECK(scratch(c, 8, 48ull * n_pk, &a));
+        HBG_CHECK(scratch(c, 8, 48ull * (n_pk ? n_pk : 1), &a));
         HBG_CHECK(scratch(c, 9, 48ull * n, &b));
         HBG_CHECK(scratch(c, 10, 8ull * n, &s1));
         HBG_CHECK(scratch(c, 11, n, &o));
         s2 = (uint8_t*)s1 + 4ull * n;
-        HBG_TRY(hipMemcpyAsync(a, pk48, 48ull * n_pk, hipMemcpyHostToDevice, c->stream));
+        if (n_pk) HBG_TRY(hipMemcpyAsync(a, pk48, 48ull * n_pk, hipMemcpyHostToDevice, c->stream));
         HBG_TRY(hipMemcpyAsync(b, share48, 48ull * n, hipMemcpyHostToDevice, c->stream));
         HBG_TRY(hipMemcpyAsync(s1, share_ct, 4ull * n, hipMemcpyHostToDevice, c->stream));
         HBG_TRY(hipMemcpyAsync(s2, share_pk, 4ull * n, hipMemcpyHostToDevice, c->stream));
@@ -676,22 +685,28 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
         dsc = (const uint32_t*)s1;
         dsp = (const uint32_t*)s2;
         dok = (uint8_t*)o;
+    } else {
+        // device mode: out-of-range (ct, pk) pairs -> the sentinels (ok = 0) + HBG_E_ARG
+        void* san;
+        HBG_CHECK(scratch(c, 29, 8ull * n, &san));
+        uint32_t* sc2 = (uint32_t*)san;
+        uint32_t* sp2 = sc2 + n;
+        HBG_TRY(bls::launch_tdec_index_sanitize(n, share_ct, n_ct, share_pk, n_pk, sc2, sp2, c->d_err, c->stream));
+        dsc = sc2;
+        dsp = sp2;
     }
     void *paff, *pst;
-    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
-    HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
-    HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    HBG_CHECK(prepare_pks(c, n_pk, dpk, &paff, &pst));
     if (c->tdec_batched && n >= 2 && n < (1ull << 31)) {
         HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, n_pk, dsh, dsc, dsp, (const uint32_t*)paff,
                                         (const int32_t*)pst, dok));
     } else {
-        HBG_TRY(bls::launch_tdec_verify_shares(n, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW,
+        HBG_TRY(bls::launch_tdec_verify_shares(n, nullptr, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW,
                                                (uint32_t*)paff, (int32_t*)pst, dok, c->stream));
     }
     if (!(flags & HBG_DEVICE)) {
         HBG_TRY(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, c->stream));
-        HBG_TRY(hipStreamSynchronize(c->stream));
-        return HBG_OK;
+        return sync_status(c);
     }
     return finish(c, flags);
 }
@@ -700,6 +715,7 @@ int hbg_ct_verify(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* 
                   const uint8_t* W96, uint8_t* ok, uint32_t flags) {
     if (!c || (n_ct && (!U48 || !V_off || !W96 || !ok))) return HBG_E_ARG;
     if (n_ct == 0) return HBG_OK;
+    if (n_ct == 0xFFFFFFFFu) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     CtTable t;
@@ -715,8 +731,7 @@ int hbg_ct_verify(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* 
     HBG_TRY(bls::launch_tdec_ct_verify(n_ct, t.ct_u, t.ct_status, t.coefH, t.coefW, dok, c->stream));
     if (!(flags & HBG_DEVICE)) {
         HBG_TRY(hipMemcpyAsync(ok, dok, n_ct, hipMemcpyDeviceToHost, c->stream));
-        HBG_TRY(hipStreamSynchronize(c->stream));
-        return HBG_OK;
+        return sync_status(c);
     }
     return finish(c, flags);
 }
@@ -725,6 +740,7 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
                      const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status, uint32_t flags) {
     if (!c || (n_ct && (!share48 || !idx || !V_off || !out || !status))) return HBG_E_ARG;
     if (n_ct == 0) return HBG_OK;
+    if (t >= 4096) return HBG_E_ARG;  // far beyond any N <= 65536 network; bounds the per-lane scratch
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t m = (uint64_t)t + 1;
@@ -760,8 +776,7 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
     if (!(flags & HBG_DEVICE)) {
         if (vlen) HBG_TRY(hipMemcpyAsync(out, dout, vlen, hipMemcpyDeviceToHost, c->stream));
         HBG_TRY(hipMemcpyAsync(status, dst, 4ull * n_ct, hipMemcpyDeviceToHost, c->stream));
-        HBG_TRY(hipStreamSynchronize(c->stream));
-        return HBG_OK;
+        return sync_status(c);
     }
     return finish(c, flags);
 }
@@ -791,14 +806,7 @@ int drain(hbg_ctx* c, uint32_t flags, std::initializer_list<std::pair<void*, std
     if (flags & HBG_DEVICE) return finish(c, flags);
     for (auto& o : outs)
         if (o.second.second) HBG_TRY(hipMemcpyAsync(o.first, o.second.first, o.second.second, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
-}
-bool index_ok(uint32_t flags, const uint32_t* idx, uint64_t n, uint64_t bound) {
-    if (flags & HBG_DEVICE) return true;  // device indices are the caller's contract
-    for (uint64_t k = 0; k < n; ++k)
-        if (idx[k] >= bound) return false;
-    return true;
+    return sync_status(c);
 }
 constexpr uint64_t kVerifyChunk = 131072;  // messages per bls_verify launch (G2Prepared scratch: 39 KB each)
 }  // namespace
@@ -818,8 +826,8 @@ int hbg_bls_sign(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_t n, con
     HBG_CHECK(stage_in(c, flags, 2, msg, mlen, &dm));
     HBG_CHECK(stage_in(c, flags, 3, msg_off, 8ull * (n + 1), &doff));
     HBG_CHECK(stage_out(c, flags, 4, sig96, 96ull * n, &dsig));
-    HBG_TRY(bls::launch_bls_sign(n, (const uint8_t*)dsk, (const uint32_t*)dms, (const uint8_t*)dm,
-                                 (const uint64_t*)doff, (uint8_t*)dsig, c->stream));
+    HBG_TRY(bls::launch_bls_sign(n, n_sk, (const uint8_t*)dsk, (const uint32_t*)dms, (const uint8_t*)dm,
+                                 (const uint64_t*)doff, (uint8_t*)dsig, c->d_err, c->stream));
     return drain(c, flags, {{sig96, {dsig, 96ull * n}}});
 }
 
@@ -839,17 +847,15 @@ int hbg_bls_verify(hbg_ctx* c, uint32_t n_pk, const uint8_t* pk48, uint64_t n, c
     HBG_CHECK(stage_in(c, flags, 3, msg_off, 8ull * (n + 1), &doff));
     HBG_CHECK(stage_in(c, flags, 9, sig96, 96ull * n, &dsig));
     HBG_CHECK(stage_out(c, flags, 4, ok, n, &dok));
-    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
-    HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
     const uint64_t chunk = n < kVerifyChunk ? n : kVerifyChunk;
     HBG_CHECK(scratch(c, 6, 8ull * bls::kLineWordsPerPoint * chunk, &lines));
-    HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    HBG_CHECK(prepare_pks(c, n_pk, (const uint8_t*)dpk, &paff, &pst));
     for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
         const uint64_t m = (n - k0) < chunk ? (n - k0) : chunk;
-        HBG_TRY(bls::launch_bls_verify(m, (const uint32_t*)paff, (const int32_t*)pst, (const uint32_t*)dmp + k0,
+        HBG_TRY(bls::launch_bls_verify(m, n_pk, (const uint32_t*)paff, (const int32_t*)pst, (const uint32_t*)dmp + k0,
                                        (const uint8_t*)dm, (const uint64_t*)doff + k0,
                                        (const uint8_t*)dsig + 96ull * k0, (uint32_t*)lines, (uint8_t*)dok + k0,
-                                       c->stream));
+                                       c->d_err, c->stream));
     }
     return drain(c, flags, {{ok, {dok, n}}});
 }
@@ -871,15 +877,11 @@ int hbg_tdec_encrypt(hbg_ctx* c, const uint8_t* pk48, uint64_t n, const uint8_t*
     HBG_CHECK(stage_out(c, flags, 4, U48, 48ull * n, &dU));
     HBG_CHECK(stage_out(c, flags, 5, V, mlen, &dV));
     HBG_CHECK(stage_out(c, flags, 9, W96, 96ull * n, &dW));
-    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords, &paff));
-    HBG_CHECK(scratch(c, 13, 4, &pst));
-    HBG_TRY(bls::launch_tdec_pk_prepare(1, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
-    int32_t hst = 0;
-    HBG_TRY(hipMemcpyAsync(&hst, pst, 4, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    if (hst != 0) return HBG_E_INVALID_POINT;
-    HBG_TRY(bls::launch_tdec_encrypt(n, (const uint32_t*)paff, (const uint8_t*)dr, (const uint8_t*)dm,
-                                     (const uint64_t*)doff, (uint8_t*)dU, (uint8_t*)dV, (uint8_t*)dW, c->stream));
+    HBG_CHECK(prepare_pks(c, 1, (const uint8_t*)dpk, &paff, &pst));
+    // an undecodable pk: HBG_E_INVALID_POINT from the kernel (returned at the next synchronisation point)
+    HBG_TRY(bls::launch_tdec_encrypt(n, (const uint32_t*)paff, (const int32_t*)pst, (const uint8_t*)dr,
+                                     (const uint8_t*)dm, (const uint64_t*)doff, (uint8_t*)dU, (uint8_t*)dV,
+                                     (uint8_t*)dW, c->d_err, c->stream));
     return drain(c, flags, {{U48, {dU, 48ull * n}}, {V, {dV, mlen}}, {W96, {dW, 96ull * n}}});
 }
 
@@ -900,12 +902,10 @@ int hbg_tdec_decrypt_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, uint3
     HBG_CHECK(stage_in(c, flags, 3, share_sk, 4ull * n, &dss));
     HBG_CHECK(stage_out(c, flags, 4, share48, 48ull * n, &dsh));
     HBG_CHECK(stage_out(c, flags, 5, status, 4ull * n, &dst));
-    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_ct, &uaff));
-    HBG_CHECK(scratch(c, 13, 4ull * n_ct, &ust));
-    HBG_TRY(bls::launch_tdec_pk_prepare(n_ct, (const uint8_t*)dU, (uint32_t*)uaff, (int32_t*)ust, c->stream));
-    HBG_TRY(bls::launch_tdec_decrypt_share(n, (const uint32_t*)uaff, (const int32_t*)ust, (const uint8_t*)dsk,
-                                           (const uint32_t*)dsc, (const uint32_t*)dss, (uint8_t*)dsh,
-                                           (int32_t*)dst, c->stream));
+    HBG_CHECK(prepare_pks(c, n_ct, (const uint8_t*)dU, &uaff, &ust));
+    HBG_TRY(bls::launch_tdec_decrypt_share(n, n_ct, n_sk, (const uint32_t*)uaff, (const int32_t*)ust,
+                                           (const uint8_t*)dsk, (const uint32_t*)dsc, (const uint32_t*)dss,
+                                           (uint8_t*)dsh, (int32_t*)dst, c->d_err, c->stream));
     return drain(c, flags, {{share48, {dsh, 48ull * n}}, {status, {dst, 4ull * n}}});
 }
 
@@ -913,7 +913,7 @@ int hbg_sig_combine(hbg_ctx* c, uint32_t t, uint64_t n, const uint8_t* share96, 
                     uint8_t* sig96, uint8_t* parity, int32_t* status, uint32_t flags) {
     if (!c || (n && (!share96 || !share_index || !sig96 || !parity || !status))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    if (t + 1 > 32) return HBG_E_ARG;  // one 32-lane group per coin
+    if (t >= 32) return HBG_E_ARG;  // one 32-lane group per coin: t + 1 <= 32
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t m = (uint64_t)t + 1;
@@ -930,41 +930,7 @@ int hbg_sig_combine(hbg_ctx* c, uint32_t t, uint64_t n, const uint8_t* share96, 
 }
 
 namespace {
-constexpr uint32_t kSigCheckChunk = 131072;  // check items / shares per launch (G2Prepared scratch: 19.6 KB each)
 constexpr uint64_t kSigSpecItems = 131072;   // 2 waves per SIMD of 256 CUs x 4 SIMDs x 64 lanes
-
-// One check round over n_items items (device list `items`, or every batch
-// when null), chunked so the per-lane G2Prepared scratch stays bounded.
-int sig_check_round(hbg_ctx* c, uint32_t n_items, uint32_t spec, const bls::CheckItem* items,
-                    const bls::BatchDesc* desc,
-                    const uint32_t* perm, const uint32_t* sums, const uint8_t* lok, const uint32_t* coefH,
-                    uint8_t* dok, bls::CheckItem* next, uint32_t* next_n, uint32_t* fails, uint32_t* fail_n) {
-    if (n_items == 0) return HBG_OK;
-    const uint32_t chunk = n_items < kSigCheckChunk ? n_items : kSigCheckChunk;
-    void* lines;
-    HBG_CHECK(scratch(c, 14, 4ull * bls::kLineWordsPerPoint * chunk, &lines));
-    for (uint32_t i0 = 0; i0 < n_items; i0 += chunk) {
-        const uint32_t m = (n_items - i0) < chunk ? (n_items - i0) : chunk;
-        HBG_TRY(bls::launch_sig_batch_check(m, i0, spec, items, desc, perm, sums, lok, coefH, (uint32_t*)lines, dok, next,
-                                            next_n, fails, fail_n, c->stream));
-    }
-    return HBG_OK;
-}
-
-int sig_verify_sel(hbg_ctx* c, uint64_t n, const uint32_t* sel, const uint8_t* dsh, const uint32_t* dsd,
-                   const uint32_t* dsp, const uint32_t* paff, const int32_t* pst, const uint32_t* coefH,
-                   uint8_t* dok) {
-    if (n == 0) return HBG_OK;
-    const uint64_t chunk = n < kSigCheckChunk ? n : kSigCheckChunk;
-    void* lines;
-    HBG_CHECK(scratch(c, 14, 4ull * bls::kLineWordsPerPoint * chunk, &lines));
-    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
-        const uint64_t m = (n - k0) < chunk ? (n - k0) : chunk;
-        HBG_TRY(bls::launch_sig_verify_shares(m, k0, sel, dsh, dsd, dsp, paff, pst, coefH, (uint32_t*)lines, dok,
-                                              c->stream));
-    }
-    return HBG_OK;
-}
 }  // namespace
 
 int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const uint64_t* doc_off, uint32_t n_pk,
@@ -973,12 +939,13 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
     if (!c || (n && (!doc_off || !pk48 || !share96 || !share_doc || !share_pk || !ok || n_pk == 0 || n_doc == 0)))
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
+    if (n_doc == 0xFFFFFFFFu || n_pk == 0xFFFFFFFFu) return HBG_E_ARG;  // the sentinels need one more index
     if (!index_ok(flags, share_doc, n, n_doc) || !index_ok(flags, share_pk, n, n_pk)) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t dlen = (flags & HBG_DEVICE) ? 0 : doc_off[n_doc];
     const void *dpk, *dd, *doff, *dsh, *dsd, *dsp;
-    void *dok, *paff, *pst, *coefH, *seeds;
+    void *dok, *paff, *pst, *coefH, *seeds, *lines;
     HBG_CHECK(stage_in(c, flags, 0, pk48, 48ull * n_pk, &dpk));
     HBG_CHECK(stage_in(c, flags, 1, share_doc, 4ull * n, &dsd));
     HBG_CHECK(stage_in(c, flags, 2, doc, dlen, &dd));
@@ -986,23 +953,35 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
     HBG_CHECK(stage_in(c, flags, 9, share96, 96ull * n, &dsh));
     HBG_CHECK(stage_in(c, flags, 10, share_pk, 4ull * n, &dsp));
     HBG_CHECK(stage_out(c, flags, 4, ok, n, &dok));
-    HBG_CHECK(scratch(c, 12, 4ull * bls::kAffWords * n_pk, &paff));
-    HBG_CHECK(scratch(c, 13, 4ull * n_pk, &pst));
+    if (flags & HBG_DEVICE) {  // out-of-range (doc, pk) pairs -> the sentinels (ok = 0) + HBG_E_ARG
+        void* san;
+        HBG_CHECK(scratch(c, 29, 8ull * n, &san));
+        uint32_t* sd2 = (uint32_t*)san;
+        uint32_t* sp2 = sd2 + n;
+        HBG_TRY(bls::launch_tdec_index_sanitize(n, (const uint32_t*)dsd, n_doc, (const uint32_t*)dsp, n_pk, sd2, sp2,
+                                                c->d_err, c->stream));
+        dsd = sd2;
+        dsp = sp2;
+    }
+    HBG_CHECK(prepare_pks(c, n_pk, (const uint8_t*)dpk, &paff, &pst));
     HBG_CHECK(scratch(c, 7, 4ull * bls::kLineWordsPerPoint * n_doc, &coefH));
     HBG_CHECK(scratch(c, 8, 32ull * n_doc, &seeds));
-    HBG_TRY(bls::launch_tdec_pk_prepare(n_pk, (const uint8_t*)dpk, (uint32_t*)paff, (int32_t*)pst, c->stream));
+    HBG_CHECK(scratch(c, 14, 4ull * bls::kLineWordsPerPoint * bls::kResidentBlocks * 64, &lines));
     HBG_TRY(bls::launch_sig_doc_prepare(n_doc, (const uint8_t*)dd, (const uint64_t*)doff, (uint32_t*)coefH,
                                         (uint8_t*)seeds, c->stream));
     const uint32_t *sd = (const uint32_t*)dsd, *sp = (const uint32_t*)dsp, *pa = (const uint32_t*)paff;
     const int32_t* ps = (const int32_t*)pst;
     const uint8_t* sh = (const uint8_t*)dsh;
     uint8_t* o = (uint8_t*)dok;
+    const uint32_t* ch = (const uint32_t*)coefH;
     if (!(c->tdec_batched && n >= 2 && n < (1ull << 31))) {
-        HBG_CHECK(sig_verify_sel(c, n, nullptr, sh, sd, sp, pa, ps, (const uint32_t*)coefH, o));
+        HBG_TRY(bls::launch_sig_verify_shares(n, nullptr, nullptr, sh, sd, sp, pa, ps, ch, (uint32_t*)lines, o,
+                                              c->stream));
         return drain(c, flags, {{ok, {dok, n}}});
     }
-    // batched: sort by document, batches of <= 64, weighted sums, 4-ary group testing
-    const uint32_t nn = (uint32_t)n;
+    // batched: sort by document, batches of <= 64, weighted sums, 4-ary group
+    // testing; every round's count is a device word (no host round trip)
+    const uint32_t nn = (uint32_t)n, n_keys = n_doc + 1;
     uint32_t* tbl = nullptr;
     if (c->tdec_batched == 2 || n >= kPkTableMinUses * n_pk) {
         void* p;
@@ -1019,55 +998,50 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
     HBG_CHECK(scratch(c, 20, (size_t)bls::kBatchDescBytes * n, &desc));
     HBG_CHECK(scratch(c, 21, tb_bytes, &temp));
     HBG_CHECK(scratch(c, 22, 64, &cnt));
-    uint32_t nbh[2] = {0, 0};
-    HBG_TRY(bls::launch_tdec_batch_plan(nn, n_doc, sd, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta,
-                                        (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, nbh, c->stream));
-    const uint32_t nb = nbh[0] + nbh[1];
+    const uint32_t nb = bls::tdec_batch_bound(nn, n_keys);
     void *sums, *lok, *items, *items2, *fails;
     HBG_CHECK(scratch(c, 23, (size_t)bls::kSigBatchSumBytes * nb, &sums));
     HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
     HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 4 * nb, &items));
     HBG_CHECK(scratch(c, 28, (size_t)bls::kCheckItemBytes * 16 * nb, &items2));
     HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
-    uint32_t* counts = (uint32_t*)cnt;  // [0] 16-group items, [1] failing shares, [2] quad items
+    uint32_t* counts = (uint32_t*)cnt;  // [0] 16-group items, [1] failing shares, [2] quad items, [3] batches
     const bls::BatchDesc* ds = (const bls::BatchDesc*)desc;
-    const uint32_t *pm = (const uint32_t*)perm, *sm = (const uint32_t*)sums, *ch = (const uint32_t*)coefH;
+    const uint32_t *pm = (const uint32_t*)perm, *sm = (const uint32_t*)sums;
     const uint8_t* lk = (const uint8_t*)lok;
+    uint32_t* ln = (uint32_t*)lines;
+    auto* it1 = (bls::CheckItem*)items;
+    auto* it2 = (bls::CheckItem*)items2;
+    HBG_TRY(hipMemsetAsync(counts, 0, 12, c->stream));
+    HBG_TRY(bls::launch_tdec_batch_plan(nn, n_keys, sd, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta,
+                                        (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, counts + 3, c->stream));
     HBG_TRY(hipMemsetAsync(o, 0, n, c->stream));
-    HBG_TRY(hipMemsetAsync(counts, 0, 16, c->stream));
-    HBG_TRY(bls::launch_sig_batch_leaves(nb, ds, pm, sh, sp, (const uint8_t*)seeds, pa, ps, tbl, (uint32_t*)sums,
-                                         (uint8_t*)lok, c->stream));
-    uint32_t h[3];
+    HBG_TRY(bls::launch_sig_batch_leaves(nb, counts + 3, n_doc, ds, pm, sh, sp, (const uint8_t*)seeds, pa, ps, tbl,
+                                         (uint32_t*)sums, (uint8_t*)lok, c->stream));
     // Check rounds run one pairing per lane and are latency-bound below ~1 wave
     // per SIMD; while 5 items per batch still fit one such wave per SIMD, the
-    // 16-groups are checked speculatively in round 0 (one round fewer).
-    // (test mode 2 always takes the plain rounds so both schedules stay covered)
-    const bool spec = c->tdec_batched != 2 && (uint64_t)nb * 5u <= kSigSpecItems;
+    // 16-groups are checked speculatively in round 0 (one round fewer).  The
+    // decision uses the full-batch estimate n / 64 (the exact count is a device
+    // word).  Test mode 2 always takes the plain rounds so both stay covered.
+    const uint64_t nb_est = nn / bls::kBatchShares ? nn / bls::kBatchShares : 1;
+    const bool spec = c->tdec_batched != 2 && nb_est * 5u <= kSigSpecItems;
     if (spec) {
-        HBG_CHECK(sig_check_round(c, nb * 5u, 1, nullptr, ds, pm, sm, lk, ch, o, (bls::CheckItem*)items2, counts + 2,
-                                  (uint32_t*)fails, counts + 1));
+        HBG_TRY(bls::launch_sig_batch_check(nb, counts + 3, 1, nullptr, ds, pm, sm, lk, ch, ln, o, it2, counts + 2,
+                                            (uint32_t*)fails, counts + 1, c->stream));
     } else {
         // round 0: every batch; failing batches push their 16-share groups
-        HBG_CHECK(sig_check_round(c, nb, 0, nullptr, ds, pm, sm, lk, ch, o, (bls::CheckItem*)items, counts,
-                                  (uint32_t*)fails, counts + 1));
-        HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
-        HBG_TRY(hipStreamSynchronize(c->stream));
+        HBG_TRY(bls::launch_sig_batch_check(nb, counts + 3, 0, nullptr, ds, pm, sm, lk, ch, ln, o, it1, counts,
+                                            (uint32_t*)fails, counts + 1, c->stream));
         // round 1: 16-share groups; failing ones push their quads
-        HBG_CHECK(sig_check_round(c, h[0], 0, (const bls::CheckItem*)items, ds, pm, sm, lk, ch, o,
-                                  (bls::CheckItem*)items2, counts + 2, (uint32_t*)fails, counts + 1));
+        HBG_TRY(bls::launch_sig_batch_check(4 * nb, counts, 0, it1, ds, pm, sm, lk, ch, ln, o, it2, counts + 2,
+                                            (uint32_t*)fails, counts + 1, c->stream));
     }
-    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
     // round 2: quads; failing ones append their shares
-    HBG_CHECK(sig_check_round(c, h[2], 0, (const bls::CheckItem*)items2, ds, pm, sm, lk, ch, o, nullptr, nullptr,
-                              (uint32_t*)fails, counts + 1));
-    HBG_TRY(hipMemcpyAsync(h, counts, 12, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    if (getenv("HBG_TDEC_DEBUG"))
-        fprintf(stderr, "hbg batched sig verify: n=%u batches=%u 16-groups=%u quads=%u fail-shares=%u\n", nn, nb,
-                h[0], h[2], h[1]);
+    HBG_TRY(bls::launch_sig_batch_check(16 * nb, counts + 2, 0, it2, ds, pm, sm, lk, ch, ln, o, nullptr, nullptr,
+                                        (uint32_t*)fails, counts + 1, c->stream));
     // round 3: the shares of failing quads, one by one (the reference's equation)
-    HBG_CHECK(sig_verify_sel(c, h[1], (const uint32_t*)fails, sh, sd, sp, pa, ps, ch, o));
+    HBG_TRY(bls::launch_sig_verify_shares(n, counts + 1, (const uint32_t*)fails, sh, sd, sp, pa, ps, ch, ln, o,
+                                          c->stream));
     return drain(c, flags, {{ok, {dok, n}}});
 }
 
@@ -1093,8 +1067,7 @@ int hbg_test_bls(hbg_ctx* c, int op, uint32_t n, const uint32_t* in, uint32_t in
     HBG_TRY(bls::launch_tdec_test(op, n, (const uint32_t*)di, (uint32_t*)dout, in_words, out_words, (uint32_t*)dl,
                                   c->stream));
     HBG_TRY(hipMemcpyAsync(out, dout, 4ull * out_words * n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 uint32_t hbg_proof_digests(uint32_t N, uint32_t index) { return host_proof_digests(N, index); }
@@ -1116,7 +1089,7 @@ int hbg_rbc_write_proof_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* 
     if (flags & HBG_DEVICE) {
         if (stride % 16 || !aligned(shards, 16) || !aligned(out, 16)) return HBG_E_ARG;
         HBG_TRY(launch_rbc_write_proof_msgs(N, L, shards, stride, levels, n, tag, m, inst, index, out, out_off,
-                                           c->stream));
+                                           c->d_err, c->stream));
         return finish(c, flags);
     }
     std::vector<uint64_t> off(m + 1);
@@ -1141,10 +1114,9 @@ int hbg_rbc_write_proof_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* 
     HBG_TRY(hipMemcpyAsync(doff, off.data(), 8 * (m + 1), hipMemcpyHostToDevice, c->stream));
     HBG_TRY(launch_rbc_write_proof_msgs(N, L, (const uint8_t*)dsh, S, (const uint8_t*)dlev, n, tag, m,
                                        (const uint64_t*)dinst, (const uint32_t*)didx, (uint8_t*)dout,
-                                       (const uint64_t*)doff, c->stream));
+                                       (const uint64_t*)doff, c->d_err, c->stream));
     HBG_TRY(hipMemcpyAsync(out + out_off[0], dout, total, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 int hbg_rbc_read_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* msgs, const uint64_t* msg_off, uint64_t m,
@@ -1190,8 +1162,7 @@ int hbg_rbc_read_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* msgs, c
     HBG_TRY(hipMemcpyAsync(ndig, dnd, 4 * m, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpyAsync(roots, drt, 32 * m, hipMemcpyDeviceToHost, c->stream));
     HBG_TRY(hipMemcpyAsync(status, dst, 4 * m, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 uint64_t hbg_wire_frame_len(uint64_t msg_len) { return 4 + 8 + msg_len + 96; }
@@ -1202,13 +1173,12 @@ int hbg_wire_sign_frames(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_
     if (!c || (n && (!sk32 || !msg_sk || !msg_off || !frames || !frame_off || n_sk == 0))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
     if (!index_ok(flags, msg_sk, n, n_sk)) return HBG_E_ARG;
-    uint64_t max_len = 0;
     if (!(flags & HBG_DEVICE)) {
         for (uint64_t k = 0; k < n; ++k) {
             if (msg_off[k + 1] < msg_off[k] || frame_off[k + 1] < frame_off[k]) return HBG_E_ARG;
             const uint64_t len = msg_off[k + 1] - msg_off[k];
             if (frame_off[k + 1] - frame_off[k] != hbg_wire_frame_len(len)) return HBG_E_ARG;
-            if (len > max_len) max_len = len;
+            if (8 + len + 96 > HBG_WIRE_MAX_FRAME) return HBG_E_WIRE_FRAME;  // FramedWrite: frame too big
         }
         if (msg_off[n] && !msg) return HBG_E_ARG;
     }
@@ -1225,15 +1195,10 @@ int hbg_wire_sign_frames(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_
     HBG_CHECK(scratch(c, 4, 96ull * n, &dsig));
     const uint64_t* dfoff;
     if (flags & HBG_DEVICE) {
+        // frame sizes are checked by the pack kernel in device mode (a wrong-size or oversized
+        // frame stays unwritten and flags HBG_E_ARG / HBG_E_WIRE_FRAME)
         dfr = frames;
         dfoff = frame_off;
-        // frame sizes are the caller's contract in device mode (the pack kernel skips frames of the
-        // wrong size); the grid is sized for the longest message, read from the (small) offsets
-        std::vector<uint64_t> h(n + 1);
-        HBG_TRY(hipMemcpyAsync(h.data(), msg_off, 8ull * (n + 1), hipMemcpyDeviceToHost, c->stream));
-        HBG_TRY(hipStreamSynchronize(c->stream));
-        for (uint64_t k = 0; k < n; ++k)
-            if (h[k + 1] > h[k] && h[k + 1] - h[k] > max_len) max_len = h[k + 1] - h[k];
     } else {
         std::vector<uint64_t> off(n + 1);
         for (uint64_t k = 0; k <= n; ++k) off[k] = frame_off[k] - frame_off[0];
@@ -1242,14 +1207,13 @@ int hbg_wire_sign_frames(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_
         HBG_TRY(hipMemcpyAsync(dfo, off.data(), 8ull * (n + 1), hipMemcpyHostToDevice, c->stream));
         dfoff = (const uint64_t*)dfo;
     }
-    HBG_TRY(bls::launch_bls_sign(n, (const uint8_t*)dsk, (const uint32_t*)dms, (const uint8_t*)dm,
-                                 (const uint64_t*)doff, (uint8_t*)dsig, c->stream));
+    HBG_TRY(bls::launch_bls_sign(n, n_sk, (const uint8_t*)dsk, (const uint32_t*)dms, (const uint8_t*)dm,
+                                 (const uint64_t*)doff, (uint8_t*)dsig, c->d_err, c->stream));
     HBG_TRY(launch_wire_frame_pack(n, (const uint8_t*)dm, (const uint64_t*)doff, (const uint8_t*)dsig,
-                                   (uint8_t*)dfr, dfoff, max_len, c->stream));
+                                   (uint8_t*)dfr, dfoff, c->d_err, c->stream));
     if (flags & HBG_DEVICE) return finish(c, flags);
     HBG_TRY(hipMemcpyAsync(frames + frame_off[0], dfr, flen, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 int hbg_wire_verify_frames(hbg_ctx* c, uint32_t n_pk, const uint8_t* pk48, uint64_t n, const uint32_t* frame_pk,
@@ -1307,8 +1271,7 @@ int hbg_synth_bytes(hbg_ctx* c, uint32_t tag, uint64_t first, uint64_t nbytes, u
     HBG_CHECK(scratch(c, 0, OS * n, &d));
     HBG_TRY(launch_synth(tag, first, nbytes, (uint8_t*)d, OS, n, c->stream));
     HBG_TRY(hipMemcpy2DAsync(out, ostride, d, OS, nbytes, n, hipMemcpyDeviceToHost, c->stream));
-    HBG_TRY(hipStreamSynchronize(c->stream));
-    return HBG_OK;
+    return sync_status(c);
 }
 
 }  // extern "C"

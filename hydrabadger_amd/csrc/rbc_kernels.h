@@ -5,8 +5,18 @@
 #include <stdint.h>
 
 #include "../../include/hbgpu.h"
+#include "dev_err.h"
 
 namespace hbg {
+
+// send_shards' layout precondition of hbg_rbc_encode_merkle: payload k maps to
+// shard_len L (hbg_shard_len(D + Q, P) == L) and fits its row (P <= stride,
+// the u32 length prefix).  Checked on the host in host mode and by
+// rbc_check_plen (+ every encode kernel, which skips such an instance) in
+// device mode.
+__host__ __device__ inline bool payload_fits(uint64_t P, uint64_t pstride, uint32_t D, uint64_t L) {
+    return P <= pstride && P <= 0xFFFFFFFFull && (P + 4 + D - 1) / D == L;
+}
 
 // Per-instance coding plan consumed by rs_code_generic:
 // out_row[out_idx[o]] = XOR_j coef[o][j] * row[in_idx[j]],  coef follows the
@@ -61,6 +71,10 @@ hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint6
                                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
 hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,
                             const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
+hipError_t launch_rbc_check_plen(uint64_t n, const uint64_t* plen, uint64_t pstride, uint32_t D, uint64_t L,
+                                 int32_t* err, hipStream_t st);
+hipError_t launch_rbc_trivial_status(uint64_t n, uint32_t N, const uint8_t* present, int32_t* status,
+                                     hipStream_t st);
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st);
 hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint64_t n, const uint8_t* matrix,
@@ -77,13 +91,13 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
 hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* shards, uint64_t S,
                                        const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m,
                                        const uint64_t* inst, const uint32_t* index, uint8_t* out,
-                                       const uint64_t* out_off, hipStream_t st);
+                                       const uint64_t* out_off, int32_t* err, hipStream_t st);
 hipError_t launch_rbc_read_msgs(uint32_t N, uint64_t L, const uint8_t* msgs, const uint64_t* msg_off, uint64_t m,
                                 uint32_t* tag, uint8_t* values, uint64_t vstride, uint32_t* index,
                                 uint8_t* digests, uint32_t* ndig, uint8_t* roots, int32_t* status, hipStream_t st);
 uint32_t host_proof_digests(uint32_t N, uint32_t i);
 hipError_t launch_wire_frame_pack(uint64_t n, const uint8_t* msg, const uint64_t* msg_off, const uint8_t* sig96,
-                                  uint8_t* frames, const uint64_t* frame_off, uint64_t max_len, hipStream_t st);
+                                  uint8_t* frames, const uint64_t* frame_off, int32_t* err, hipStream_t st);
 hipError_t launch_synth(uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride, uint64_t n,
                         hipStream_t st);
 

@@ -157,34 +157,31 @@ template <int D, int Q, bool FROM_PAYLOAD>
 __global__ __launch_bounds__(256, 4) void rs_encode_const(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                        uint64_t n, uint32_t blocks_per_inst,
                                                        const uint8_t* __restrict__ payloads, uint64_t pstride,
-                                                       const uint64_t* __restrict__ plen, uint32_t order) {
-    // order bit 0: XCD-aware block numbering (the G/8 logical blocks an XCD
-    // receives are consecutive, so neighbouring 1-KiB slices of a row share
-    // that XCD's L2); bits 8..15: R slices per block (R = 0 means 1).
-    const uint32_t R = ((order >> 8) & 0xff) ? ((order >> 8) & 0xff) : 1;
-    const uint32_t lb = (order & 1) ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t bpr = (blocks_per_inst + R - 1) / R;
-    const uint64_t inst = lb / bpr;
+                                                       const uint64_t* __restrict__ plen) {
+    // XCD-aware block numbering: the G/8 logical blocks an XCD receives are
+    // consecutive, so neighbouring 1-KiB slices of a row share that XCD's L2
+    // (8,192 x 1 MiB: 35.6 -> 34.1 GB of HBM traffic).
+    const uint32_t lb = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t inst = lb / blocks_per_inst;
     if (inst >= n) return;
     uint8_t* base = shards + inst * (uint64_t)(D + Q) * S;
-    for (uint32_t k = 0; k < R; ++k) {
-        const uint32_t blk = (lb % bpr) * R + k;
-        const uint32_t p = blk * 256 + threadIdx.x;
-        if constexpr (FROM_PAYLOAD) {
-            const uint8_t* pay = payloads + inst * pstride;
-            const uint64_t P = plen[inst];
-            const uint64_t end = 4 * (uint64_t)(blk * 256 + 256);  // value-byte end of this block in a row
-            // interior: past the length prefix, inside the row, and the last row's
-            // dwordx2 window [.., (D-1)L + end + 4) inside the payload (+4 prefix)
-            const bool interior = blk > 0 && end <= L && (uint64_t)(D - 1) * L + end + 4 <= P + 4;
-            if (interior) {
-                encode_word<D, Q, 2>(base, S, L, p, pay, P);
-            } else if (4 * (uint64_t)p < L) {
-                encode_word<D, Q, 1>(base, S, L, p, pay, P);
-            }
-        } else {
-            if (4 * (uint64_t)p < L) encode_word<D, Q, 0>(base, S, L, p, nullptr, 0);
+    const uint32_t blk = lb % blocks_per_inst;
+    const uint32_t p = blk * 256 + threadIdx.x;
+    if constexpr (FROM_PAYLOAD) {
+        const uint8_t* pay = payloads + inst * pstride;
+        const uint64_t P = plen[inst];
+        if (!payload_fits(P, pstride, D, L)) return;  // device-mode argument check (flagged by rbc_check_plen)
+        const uint64_t end = 4 * (uint64_t)(blk * 256 + 256);  // value-byte end of this block in a row
+        // interior: past the length prefix, inside the row, and the last row's
+        // dwordx2 window [.., (D-1)L + end + 4) inside the payload (+4 prefix)
+        const bool interior = blk > 0 && end <= L && (uint64_t)(D - 1) * L + end + 4 <= P + 4;
+        if (interior) {
+            encode_word<D, Q, 2>(base, S, L, p, pay, P);
+        } else if (4 * (uint64_t)p < L) {
+            encode_word<D, Q, 1>(base, S, L, p, pay, P);
         }
+    } else {
+        if (4 * (uint64_t)p < L) encode_word<D, Q, 0>(base, S, L, p, nullptr, 0);
     }
 }
 
@@ -200,84 +197,51 @@ __global__ __launch_bounds__(256) void pack_rows(uint8_t* __restrict__ shards, u
     if (inst >= n || 4 * p >= L) return;
     const uint8_t* pay = payloads + inst * pstride;
     const uint64_t P = plen[inst];
+    if (!payload_fits(P, pstride, rows, L)) return;  // flagged by rbc_check_plen
     for (uint32_t j = 0; j < rows; ++j)
         reinterpret_cast<uint32_t*>(shards + (inst * N + j) * S)[p] = value_word(pay, P, (uint64_t)j * L + 4 * p);
+}
+
+// Device-mode argument check of hbg_rbc_encode_merkle (payload_fits); the
+// encode kernels skip an instance that fails it.
+__global__ __launch_bounds__(256) void rbc_check_plen(uint64_t n, const uint64_t* __restrict__ plen, uint64_t pstride,
+                                                      uint32_t D, uint64_t L, int32_t* __restrict__ err) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n && !payload_fits(plen[k], pstride, D, L)) flag_error(err, HBG_E_ARG);
+}
+
+// Coding::Trivial (N <= 3) reconstruct: every shard must be present.
+__global__ __launch_bounds__(256) void rbc_trivial_status(uint64_t n, uint32_t N, const uint8_t* __restrict__ present,
+                                                          int32_t* __restrict__ status) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int32_t st = 0;
+    for (uint32_t i = 0; i < N; ++i)
+        if (!present[k * N + i]) st = HBG_E_TOO_FEW_SHARDS_PRESENT;
+    status[k] = st;
 }
 
 // Generic coding: out_row[o] = XOR_j coef[o][j] * in_row[j] for one instance's
 // plan (see rbc_kernels.h CodePlan) — reconstruct (per-instance coefficients)
 // and encode for (D, Q) without a compile-time encoder.  Coefficients are
-// run-time but wave-uniform, so the split-nibble tables of each input word
-// go to LDS (lane-private slots, [wave][32 entries][64 lanes]: conflict-free)
-// and every (output, input) pair is two LDS lookups + one v_bitop3.  Output
-// rows are tiled kGenericTile at a time in registers.
+// run-time but wave-uniform; output rows are tiled kGenericTile at a time in
+// registers.  kGenericLds: the LDS copy of the split-nibble tables,
+// lane-private slots [wave][32 entries][64 lanes] (conflict-free).
 constexpr uint32_t kGenericLds = 4 * 32 * 64 * 4;  // 32 KiB per 256-thread block
 
-__global__ __launch_bounds__(256) void rs_code_generic(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
-                                                       uint32_t N, uint32_t D, uint64_t n,
-                                                       uint32_t blocks_per_inst, const uint8_t* __restrict__ plans,
-                                                       uint64_t plan_stride) {
-    extern __shared__ uint32_t gtab[];
-    typedef const __attribute__((address_space(4))) uint32_t* cu32;  // scalar (SMEM) loads
-    const uint64_t inst = blockIdx.x / blocks_per_inst;
-    const uint32_t p = (blockIdx.x % blocks_per_inst) * 256 + threadIdx.x;
-    if (inst >= n) return;
-    const uint32_t Q = N - D, qp = plan_qpad(Q);
-    const uint8_t* pbase = plans + inst * plan_stride;
-    const CodePlan* plan = reinterpret_cast<const CodePlan*>(pbase);
-    if (plan->status != 0) return;
-    const uint32_t n_out = plan->n_out;
-    const bool active = 4 * (uint64_t)p < L;
-    const cu32 offs = (cu32)(pbase + plan_offs_at(D, Q));
-    uint8_t* base = shards + inst * (uint64_t)N * S;
-    uint32_t* tab = gtab + (threadIdx.x >> 6) * (32 * 64) + (threadIdx.x & 63);  // entry e at tab[64 e]
-    const uint32_t tab_addr = (uint32_t)(uintptr_t)tab;                             // LDS byte address
-    tab[0] = 0u;
-    tab[16 * 64] = 0u;
-    for (uint32_t o0 = 0; o0 < n_out; o0 += kGenericTile) {
-        uint32_t acc[kGenericTile];
-#pragma unroll
-        for (int o = 0; o < (int)kGenericTile; ++o) acc[o] = 0u;
-        const uint32_t cnt = (n_out - o0) < (uint32_t)kGenericTile ? (n_out - o0) : (uint32_t)kGenericTile;
-        for (uint32_t j = 0; j < D; ++j) {
-            const uint32_t w =
-                active ? reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p] : 0u;
-            const NibPair T = nib_tables(w);
-#pragma unroll
-            for (int e = 1; e < 16; ++e) {
-                tab[64 * e] = T.lo.t[e];
-                tab[64 * (16 + e)] = T.hi.t[e];
-            }
-            const cu32 oj = offs + 2 * ((uint64_t)j * qp + o0);
-            typedef const __attribute__((address_space(3))) uint32_t* lds32;
-#pragma unroll
-            for (int o = 0; o < (int)kGenericTile; ++o)  // rows >= cnt read the zero entries
-                acc[o] = xor3u(acc[o], *(lds32)(uintptr_t)(tab_addr + oj[2 * o]),
-                               *(lds32)(uintptr_t)(tab_addr + oj[2 * o + 1]));
-        }
-        if (active) {
-#pragma unroll
-            for (int o = 0; o < (int)kGenericTile; ++o)
-                if ((uint32_t)o < cnt)
-                    reinterpret_cast<uint32_t*>(base + (uint64_t)plan->out_idx[o0 + o] * S)[p] = acc[o];
-        }
-    }
-}
-
-// Register-table variant: the 16 + 16 split-nibble combinations of each data
-// word stay in VGPRs and the wave-uniform coefficient (decoded with SALU from
-// the plan's offsets) selects them by M0-relative register addressing
-// (v_movrels): no LDS traffic, 2 selects + 1 v_bitop3 per MAC-word.
-#ifndef HBG_MOVREL_SPLIT
-#define HBG_MOVREL_SPLIT 16
-#endif
-constexpr int kMovrelSplit = HBG_MOVREL_SPLIT;
+// The 16 + 16 split-nibble combinations of each data word stay in VGPRs and
+// the wave-uniform coefficient (decoded with SALU from the plan's offsets)
+// selects them by M0-relative register addressing (v_movrels): 2 selects + 1
+// v_bitop3 per MAC-word for the first kMovrelSplit output rows of a tile; the
+// rest read an LDS copy of the tables, so the SALU/movrel and LDS pipes run
+// side by side.
+constexpr int kMovrelSplit = 16;
 __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                       uint32_t N, uint32_t D, uint64_t n,
                                                       uint32_t blocks_per_inst, const uint8_t* __restrict__ plans,
-                                                      uint64_t plan_stride, uint32_t xcd) {
+                                                      uint64_t plan_stride) {
     typedef const __attribute__((address_space(4))) uint32_t* cu32;  // scalar (SMEM) loads
-    const uint32_t lb = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t lb = xcd_block(blockIdx.x, gridDim.x);  // XCD-aware (decode 13.25 -> 13.10 ms / 2,048)
     const uint64_t inst = lb / blocks_per_inst;
     const uint32_t p = (lb % blocks_per_inst) * 256 + threadIdx.x;
     if (inst >= n) return;
@@ -465,7 +429,6 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
 // ============================================================== family 2: Merkle
 // One work-item per leaf; lanes_per_inst = next_pow2(N) (<= 256); tree levels
 // built in LDS by the owning lanes.  levels: [n][nodes][32].
-template <int IMPL>
 __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                     uint32_t N, uint32_t lpi, uint32_t nodes, uint64_t n,
                                                     uint8_t* __restrict__ levels) {
@@ -478,7 +441,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
     uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)nodes * 32);
     if (live && leaf < N) {
         uint32_t d[8];
-        sha3_256_aligned8<IMPL>(shards + (inst * N + leaf) * S, L, d);
+        sha3_256_aligned8<1>(shards + (inst * N + leaf) * S, L, d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) tree[leaf * 8 + i] = d[i];
         gout[2 * leaf] = make_uint4(d[0], d[1], d[2], d[3]);
@@ -497,7 +460,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
                     l[i] = tree[(base + 2 * leaf) * 8 + i];
                     r[i] = tree[(base + 2 * leaf + 1) * 8 + i];
                 }
-                sha3_pair<IMPL>(l, r, d);
+                sha3_pair<1>(l, r, d);
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) d[i] = tree[(base + 2 * leaf) * 8 + i];
@@ -515,7 +478,6 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
 }
 
 // Proof::validate(N) — one work-item per proof.
-template <int IMPL>
 __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len, const uint8_t* __restrict__ values,
                                                        uint64_t vstride, const uint32_t* __restrict__ index,
                                                        const uint8_t* __restrict__ digests, uint32_t depth,
@@ -525,7 +487,7 @@ __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len,
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     uint32_t d[8];
-    sha3_256_aligned8<IMPL>(values + k * vstride, len, d);
+    sha3_256_aligned8<1>(values + k * vstride, len, d);
     uint32_t li = index[k], ln = N, used = 0;
     const uint32_t nd = ndig[k];
     const uint32_t* dg = reinterpret_cast<const uint32_t*>(digests + k * (uint64_t)depth * 32);
@@ -540,8 +502,8 @@ __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len,
 #pragma unroll
             for (int i = 0; i < 8; ++i) s[i] = dg[used * 8 + i];
             ++used;
-            if (li & 1u) sha3_pair<IMPL>(s, d, d);
-            else sha3_pair<IMPL>(d, s, d);
+            if (li & 1u) sha3_pair<1>(s, d, d);
+            else sha3_pair<1>(d, s, d);
         }
         li >>= 1;
         ln = (ln + 1) >> 1;
@@ -656,44 +618,18 @@ __global__ __launch_bounds__(256) void synth_bytes(uint32_t tag, uint64_t first,
 }
 
 // ============================================================== launchers
-// Keccak implementation for the Merkle kernels: 1 = bank-allocated asm
-// (default), 0 = compiler-scheduled C round.  HBG_KECCAK_IMPL overrides (A/B
-// measurements only; both are bit-identical and covered by the parity tests).
-static int keccak_impl() {
-    static int v = [] {
-        const char* e = getenv("HBG_KECCAK_IMPL");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v;
-}
-
-// Encoder block order (see rs_encode_const): XCD-aware numbering, one slice
-// per block (measured best: 8,192 x 1 MiB encode 9.6 -> 8.8 ms; 2 or 4 slices
-// per block, nontemporal stores, and 5-6 waves/SIMD with spills were slower).
-// HBG_ENC_ORDER overrides (A/B measurements only; every order writes the same
-// bytes).
-static uint32_t encode_order() {
-    static uint32_t v = [] {
-        const char* e = getenv("HBG_ENC_ORDER");
-        return e ? (uint32_t)strtoul(e, nullptr, 0) : 1u;
-    }();
-    return v;
-}
-
 template <int D, int Q>
 static hipError_t launch_encode_const(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                       const uint8_t* payloads, uint64_t pstride, const uint64_t* plen,
                                       hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
-    const uint32_t order = encode_order();
-    const uint32_t R = ((order >> 8) & 0xff) ? ((order >> 8) & 0xff) : 1;
-    const uint64_t blocks = n * ((bpi + R - 1) / R);
+    const uint64_t blocks = n * bpi;
     if (payloads)
         rs_encode_const<D, Q, true><<<dim3((uint32_t)blocks), dim3(256), 0, st>>>(shards, S, L, n, bpi, payloads,
-                                                                                   pstride, plen, order);
+                                                                                   pstride, plen);
     else
         rs_encode_const<D, Q, false><<<dim3((uint32_t)blocks), dim3(256), 0, st>>>(shards, S, L, n, bpi, nullptr, 0,
-                                                                                    nullptr, order);
+                                                                                    nullptr);
     return hipGetLastError();
 }
 
@@ -722,23 +658,8 @@ hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N,
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
-    static const int impl = [] {
-        const char* e = getenv("HBG_GENERIC_IMPL");
-        return e ? atoi(e) : 1;
-    }();
-    // XCD-aware block numbering (decode 13.25 -> 13.10 ms / 2,048 instances);
-    // HBG_GEN_XCD=0 restores dispatch order (A/B measurements only).
-    static const uint32_t xcd = [] {
-        const char* e = getenv("HBG_GEN_XCD");
-        return e ? (uint32_t)atoi(e) : 1u;
-    }();
-    if (impl == 1) {
-        rs_code_movrel<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
-                                                                                plan_stride, xcd);
-        return hipGetLastError();
-    }
-    rs_code_generic<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
-                                                                      plan_stride);
+    rs_code_movrel<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
+                                                                            plan_stride);
     return hipGetLastError();
 }
 
@@ -757,10 +678,7 @@ hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, ui
     const uint32_t ipb = 256 / lpi;
     const uint64_t blocks = (n + ipb - 1) / ipb;
     const size_t lds = (size_t)ipb * nodes * 32;
-    if (keccak_impl() == 1)
-        merkle_build<1><<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
-    else
-        merkle_build<0><<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
+    merkle_build<<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
     return hipGetLastError();
 }
 
@@ -768,12 +686,8 @@ hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* value
                                   const uint32_t* index, const uint8_t* digests, uint32_t depth,
                                   const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
                                   hipStream_t st) {
-    if (keccak_impl() == 1)
-        merkle_validate<1><<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index,
-                                                                                   digests, depth, ndig, roots, ok, n);
-    else
-        merkle_validate<0><<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index,
-                                                                                   digests, depth, ndig, roots, ok, n);
+    merkle_validate<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index, digests,
+                                                                           depth, ndig, roots, ok, n);
     return hipGetLastError();
 }
 
@@ -789,6 +703,20 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
     const uint32_t bpi = (uint32_t)(((maxlen + 15) / 16 + 255) / 256);
     rbc_glue_copy<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, plen, status, out,
                                                                     ostride);
+    return hipGetLastError();
+}
+
+hipError_t launch_rbc_check_plen(uint64_t n, const uint64_t* plen, uint64_t pstride, uint32_t D, uint64_t L,
+                                 int32_t* err, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    rbc_check_plen<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, plen, pstride, D, L, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_rbc_trivial_status(uint64_t n, uint32_t N, const uint8_t* present, int32_t* status,
+                                     hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    rbc_trivial_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, N, present, status);
     return hipGetLastError();
 }
 

@@ -16,59 +16,73 @@ struct BatchDesc;
 struct CheckItem;
 constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 21 * 2 * 36 * 4;
 constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G2 Jacobian sums of 21 tree nodes
+// Grid-stride check rounds run on at most this many 64-lane blocks (2 waves
+// per SIMD x 1,024 SIMDs: the TDec kernels' resident limit); per-lane scratch
+// (G2Prepared lines) is sized for kResidentBlocks * 64 lanes.
+constexpr uint32_t kResidentBlocks = 2048;
 
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
                                   uint32_t* coefW, hipStream_t st);
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st);
-hipError_t launch_tdec_verify_shares(uint64_t n, const uint8_t* share48, const uint32_t* share_ct,
-                                     const uint32_t* share_pk, const uint32_t* ct_u, const int32_t* ct_status,
-                                     const uint32_t* coefH, const uint32_t* coefW, const uint32_t* pk_aff,
-                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st,
+// cap: items the grid is sized for; n_dev (nullable): the device word holding
+// the actual count (<= cap) — the group-testing rounds never round-trip a
+// count through the host.
+hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
+                                     const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
+                                     const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
+                                     const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
                                      const uint32_t* sel = nullptr);
+hipError_t launch_tdec_index_sanitize(uint64_t n, const uint32_t* a, uint32_t a_bound, const uint32_t* b,
+                                      uint32_t b_bound, uint32_t* a_out, uint32_t* b_out, int32_t* err,
+                                      hipStream_t st);
 size_t tdec_batch_temp_bytes(uint32_t n);
-hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* share_ct, uint32_t* keys,
+hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_keys, const uint32_t* share_ct, uint32_t* keys,
                                   uint32_t* perm, uint32_t* tmp_a, uint32_t* tmp_b, BatchDesc* desc, void* temp,
-                                  size_t temp_bytes, uint32_t* nb_out, hipStream_t st);
-hipError_t launch_tdec_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share48,
-                                    const uint32_t* share_pk, const uint8_t* U48, const int32_t* ct_status,
-                                    const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* pk_tbl,
-                                    uint32_t* sums, uint8_t* leaf_ok, hipStream_t st);
+                                  size_t temp_bytes, uint32_t* nb_dev, hipStream_t st);
+uint32_t tdec_batch_bound(uint32_t n, uint32_t n_keys);  // upper bound of the batch count
+hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_ct, const BatchDesc* desc,
+                                    const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
+                                    const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
+                                    const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
+                                    uint8_t* leaf_ok, hipStream_t st);
 size_t tdec_pk_table_bytes(uint32_t n_pk);
 hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st);
-hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, const BatchDesc* desc,
-                                   const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
-                                   const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
-                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
-                                   hipStream_t st);
-hipError_t launch_bls_sign(uint64_t n, const uint8_t* sk32, const uint32_t* msg_sk, const uint8_t* msg,
-                           const uint64_t* off, uint8_t* sig96, hipStream_t st);
+hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const CheckItem* items,
+                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
+                                   const uint8_t* leaf_ok, const uint32_t* ct_u, const uint32_t* coefH,
+                                   const uint32_t* coefW, uint8_t* ok, CheckItem* next, uint32_t* next_n,
+                                   uint32_t* fail_list, uint32_t* fail_n, hipStream_t st);
+hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
+                           const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st);
 hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
                                      const uint32_t* frame_pk, const uint8_t* frames, const uint64_t* off,
                                      uint32_t* lines, int32_t* status, hipStream_t st);
-hipError_t launch_bls_verify(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* msg_pk,
-                             const uint8_t* msg, const uint64_t* off, const uint8_t* sig96, uint32_t* lines,
-                             uint8_t* ok, hipStream_t st);
-hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const uint8_t* r32, const uint8_t* msg,
-                               const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96, hipStream_t st);
-hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const int32_t* u_status, const uint8_t* sk32,
-                                     const uint32_t* share_ct, const uint32_t* share_sk, uint8_t* share48,
-                                     int32_t* status, hipStream_t st);
+hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
+                             const uint32_t* msg_pk, const uint8_t* msg, const uint64_t* off, const uint8_t* sig96,
+                             uint32_t* lines, uint8_t* ok, int32_t* err, hipStream_t st);
+hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
+                               const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
+                               int32_t* err, hipStream_t st);
+hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, const uint32_t* u_aff,
+                                     const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
+                                     const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
+                                     hipStream_t st);
 hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, const uint32_t* idx, uint8_t* sig96,
                                uint8_t* parity, int32_t* status, hipStream_t st);
 hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t* off, uint32_t* coefH,
                                   uint8_t* seeds, hipStream_t st);
-hipError_t launch_sig_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share96,
-                                   const uint32_t* share_pk, const uint8_t* seeds, const uint32_t* pk_aff,
-                                   const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
-                                   uint8_t* leaf_ok, hipStream_t st);
-hipError_t launch_sig_batch_check(uint32_t n_items, uint32_t base, uint32_t spec, const CheckItem* items,
+hipError_t launch_sig_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_doc, const BatchDesc* desc,
+                                   const uint32_t* perm, const uint8_t* share96, const uint32_t* share_pk,
+                                   const uint8_t* seeds, const uint32_t* pk_aff, const int32_t* pk_status,
+                                   const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, hipStream_t st);
+hipError_t launch_sig_batch_check(uint32_t cap, const uint32_t* n_dev, uint32_t spec, const CheckItem* items,
                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
                                   const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
                                   hipStream_t st);
-hipError_t launch_sig_verify_shares(uint64_t n, uint64_t base, const uint32_t* sel, const uint8_t* share96,
+hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint32_t* sel, const uint8_t* share96,
                                     const uint32_t* share_doc, const uint32_t* share_pk, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
                                     hipStream_t st);

@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "bls.h"
+#include "dev_err.h"
 #include "keccak.h"
 #include "tdec_kernels.h"
 
@@ -36,6 +37,16 @@ namespace bls {
 #define TDEC_KERNEL __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HBG_TDEC_WPE)))
 
 #define BD __device__ __forceinline__
+
+// Work count of a grid-stride round read on the device (no host round trip
+// between the group-testing rounds): min(*n_dev, cap), or cap without n_dev.
+BD uint64_t dev_count(const uint32_t* n_dev, uint64_t cap) {
+    if (!n_dev) return cap;
+    const uint64_t v = *n_dev;
+    return v < cap ? v : cap;
+}
+BD uint64_t grid_lane() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+BD uint64_t grid_lanes() { return (uint64_t)gridDim.x * blockDim.x; }
 
 // ------------------------------------------------------------------ SHA3-256 over bytes
 BD void sha3_bytes(const uint8_t* p, uint32_t len, uint8_t out[32]) {
@@ -430,7 +441,8 @@ TDEC_KERNEL void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
     pk_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
 }
 
-TDEC_KERNEL void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ share48,
+TDEC_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restrict__ n_dev,
+                                                         const uint8_t* __restrict__ share48,
                                                          const uint32_t* __restrict__ share_ct,
                                                          const uint32_t* __restrict__ share_pk,
                                                          const uint32_t* __restrict__ ct_u,
@@ -440,10 +452,10 @@ TDEC_KERNEL void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ shar
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const int32_t* __restrict__ pk_status,
                                                          uint8_t* __restrict__ ok, const uint32_t* __restrict__ sel) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const uint64_t n = dev_count(n_dev, cap);
+    for (uint64_t i = grid_lane(); i < n; i += grid_lanes()) {
     const uint64_t k = sel ? sel[i] : i;  // sel: share indices (batched path's failing leaves)
-    const uint32_t ct = share_ct[k], pk = share_pk[k];
+    const uint32_t ct = share_ct[k], pk = share_pk[k];  // sanitised: invalid pairs point at the sentinels
     bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
     G1A s;
     if (good) good = g1_decompress(share48 + 48ull * k, s, true);
@@ -456,6 +468,24 @@ TDEC_KERNEL void tdec_verify_shares(uint64_t n, const uint8_t* __restrict__ shar
                               coefW + (uint64_t)ct * 72 * kMillerSteps, pkx, pky, !pk_inf && !w_inf);
     }
     ok[k] = good ? 1 : 0;
+    }
+}
+
+// Device-mode index check of (ciphertext/document, key) pairs: an out-of-range
+// pair is redirected to the sentinel entries (a_bound, b_bound), whose status
+// words are invalid, so its ok bit is 0 and nothing out of range is read; the
+// call's sticky error becomes HBG_E_ARG.
+__global__ __launch_bounds__(256) void tdec_index_sanitize(uint64_t n, const uint32_t* __restrict__ a,
+                                                           uint32_t a_bound, const uint32_t* __restrict__ b,
+                                                           uint32_t b_bound, uint32_t* __restrict__ a_out,
+                                                           uint32_t* __restrict__ b_out, int32_t* __restrict__ err) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t x = a[k], y = b[k];
+    const bool good = x < a_bound && y < b_bound;
+    a_out[k] = good ? x : a_bound;
+    b_out[k] = good ? y : b_bound;
+    if (!good) flag_error(err, HBG_E_ARG);
 }
 
 
@@ -575,7 +605,8 @@ BD G1 g1_mul_ab32(const Fp& px, const Fp& py, uint32_t a, uint32_t b) {
     return r;
 }
 
-TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
+TDEC_KERNEL void tdec_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t n_ct,
+                                                        const BatchDesc* __restrict__ desc,
                                                         const uint32_t* __restrict__ perm,
                                                         const uint8_t* __restrict__ share48,
                                                         const uint32_t* __restrict__ share_pk,
@@ -587,11 +618,13 @@ TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
                                                         uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= *nb_dev) return;  // grid sized for the bound; the batch count is a device word
     const BatchDesc d = desc[b];
     const uint32_t q = d.start + lane;
     const bool in = q < d.end;
     const uint32_t k = in ? perm[q] : 0u;
     const uint32_t pk = in ? share_pk[k] : 0u;
+    const bool real_ct = d.ct < n_ct;  // the sentinel batch (out-of-range indices) reads no U
     bool valid = in && ct_status[d.ct] == 0 && pk_status[pk] == 0;
     G1A s;
     if (valid) valid = g1_decompress(share48 + 48ull * k, s, true);
@@ -599,7 +632,7 @@ TDEC_KERNEL void tdec_batch_leaves(const BatchDesc* __restrict__ desc,
     // d_i = SHA3(U || S_i || pk_i), batch digest D = SHA3(d_0 || ... ),
     // r_i = SHA3(D || i)[0..8] | 1 — changing any share re-randomises every
     // weight, so shares cannot be ground against each other's weights.
-    if (in) {
+    if (in && real_ct) {
         uint8_t m[100];
         for (int i = 0; i < 48; ++i) m[i] = U48[48ull * d.ct + i];
         for (int i = 0; i < 48; ++i) m[48 + i] = share48[48ull * k + i];
@@ -704,8 +737,10 @@ BD void batch_tree_step(bool pass, const CheckItem& it, const BatchDesc& d, cons
     }
 }
 
-// One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.
-TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict__ items,
+// One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.  Items:
+// the list `items` (count *n_dev) or, with items == null, every batch
+// (count *n_dev = the batch count); grid-stride over a resident grid.
+TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, const CheckItem* __restrict__ items,
                                                        const BatchDesc* __restrict__ desc,
                                                        const uint32_t* __restrict__ perm,
                                                        const uint32_t* __restrict__ sums,
@@ -716,13 +751,13 @@ TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict_
                                                        CheckItem* __restrict__ next, uint32_t* __restrict__ next_n,
                                                        uint32_t* __restrict__ fail_list,
                                                        uint32_t* __restrict__ fail_n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_items) return;
-    const CheckItem it = items ? items[i] : CheckItem{i, kNodeBatch};
+    const uint64_t n_items = dev_count(n_dev, cap);
+    for (uint64_t i = grid_lane(); i < n_items; i += grid_lanes()) {
+    const CheckItem it = items ? items[i] : CheckItem{(uint32_t)i, kNodeBatch};
     const BatchDesc d = desc[it.b];
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
     const uint32_t l0 = node_first(it.node);
-    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;  // nothing valid to vouch for: those shares stay 0
+    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) continue;  // nothing valid to vouch for: those shares stay 0
     const uint32_t* sm = sums + (uint64_t)it.b * kBatchSumWords + it.node * kSumWords;
     const G1A a = g1_to_affine(load_jac(sm)), bb = g1_to_affine(load_jac(sm + kJacWords));
     const bool w_inf = ct_u[32ull * d.ct + 25] != 0;
@@ -730,6 +765,7 @@ TDEC_KERNEL void tdec_batch_check(uint32_t n_items, const CheckItem* __restrict_
                                      coefW + (uint64_t)d.ct * kLineWordsPerPoint, bb.x, fp_neg(bb.y),
                                      !bb.inf && !w_inf);
     batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n);
+    }
 }
 
 TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
@@ -1097,11 +1133,16 @@ BD G2A hash_g2_msg(const uint8_t* msg, uint32_t len) {
 }
 
 // SecretKey::sign(msg) = hash_g2(msg) * sk
-TDEC_KERNEL void bls_sign(uint64_t n, const uint8_t* __restrict__ sk32, const uint32_t* __restrict__ msg_sk,
-                          const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
-                          uint8_t* __restrict__ sig96) {
+TDEC_KERNEL void bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* __restrict__ sk32,
+                          const uint32_t* __restrict__ msg_sk, const uint8_t* __restrict__ msg,
+                          const uint64_t* __restrict__ off, uint8_t* __restrict__ sig96, int32_t* __restrict__ err) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
+    if (msg_sk[k] >= n_sk) {  // device-mode index check: all-zero bytes (no valid encoding), HBG_E_ARG
+        for (int i = 0; i < 96; ++i) sig96[96ull * k + i] = 0;
+        flag_error(err, HBG_E_ARG);
+        return;
+    }
     const G2A h = hash_g2_msg(msg + off[k], (uint32_t)(off[k + 1] - off[k]));
     uint32_t sk[8];
     load_scalar(sk32 + 32ull * msg_sk[k], sk);
@@ -1112,13 +1153,19 @@ TDEC_KERNEL void bls_sign(uint64_t n, const uint8_t* __restrict__ sk32, const ui
 
 // PublicKey::verify(sig, msg): e(pk, hash_g2(msg)) == e(G1, sig); the signature
 // decodes with the crate's subgroup check (SignedWireMessage deserialisation).
-TDEC_KERNEL void bls_verify(uint64_t n, const uint32_t* __restrict__ pk_aff, const int32_t* __restrict__ pk_status,
-                            const uint32_t* __restrict__ msg_pk, const uint8_t* __restrict__ msg,
-                            const uint64_t* __restrict__ off, const uint8_t* __restrict__ sig96,
-                            uint32_t* __restrict__ lines, uint8_t* __restrict__ ok) {
+TDEC_KERNEL void bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
+                            const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ msg_pk,
+                            const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
+                            const uint8_t* __restrict__ sig96, uint32_t* __restrict__ lines, uint8_t* __restrict__ ok,
+                            int32_t* __restrict__ err) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t p = msg_pk[k];
+    if (p >= n_pk) {  // device-mode index check
+        ok[k] = 0;
+        flag_error(err, HBG_E_ARG);
+        return;
+    }
     G2A sig;
     bool good = pk_status[p] == 0 && g2_decompress(sig96 + 96ull * k, sig, true);
     if (good) {
@@ -1158,9 +1205,9 @@ TDEC_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_
     int32_t st = HBG_OK;
     uint64_t mlen = 0;
     G2A sig;
+    const uint64_t head = flen < 4 ? 0 : ((uint64_t)f[0] << 24 | (uint64_t)f[1] << 16 | (uint64_t)f[2] << 8 | f[3]);
     if (flen < 4) st = HBG_E_WIRE_EOF;
-    else if (((uint64_t)f[0] << 24 | (uint64_t)f[1] << 16 | (uint64_t)f[2] << 8 | f[3]) != flen - 4)
-        st = HBG_E_WIRE_FRAME;
+    else if (head > HBG_WIRE_MAX_FRAME || head != flen - 4) st = HBG_E_WIRE_FRAME;  // codec: too big / bad framing
     else if (flen - 4 < 8) st = HBG_E_WIRE_EOF;
     else {
         mlen = wire_le(f + 4, 8);
@@ -1194,11 +1241,18 @@ TDEC_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_
 
 // PublicKey::encrypt_with_rng with r explicit: U = r G1, V = xor_with_hash(r PK, msg),
 // W = r hash_g1_g2(U, V).  V is written at the message's offsets.
-TDEC_KERNEL void tdec_encrypt(uint64_t n, const uint32_t* __restrict__ pk_aff, const uint8_t* __restrict__ r32,
-                              const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
-                              uint8_t* __restrict__ U48, uint8_t* __restrict__ V, uint8_t* __restrict__ W96) {
+TDEC_KERNEL void tdec_encrypt(uint64_t n, const uint32_t* __restrict__ pk_aff, const int32_t* __restrict__ pk_status,
+                              const uint8_t* __restrict__ r32, const uint8_t* __restrict__ msg,
+                              const uint64_t* __restrict__ off, uint8_t* __restrict__ U48, uint8_t* __restrict__ V,
+                              uint8_t* __restrict__ W96, int32_t* __restrict__ err) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
+    if (pk_status[0] != 0) {  // the public key does not decode: HBG_E_INVALID_POINT, all-zero U and W
+        for (int i = 0; i < 48; ++i) U48[48ull * k + i] = 0;
+        for (int i = 0; i < 96; ++i) W96[96ull * k + i] = 0;
+        if (k == 0) flag_error(err, HBG_E_INVALID_POINT);
+        return;
+    }
     uint32_t r[8];
     load_scalar(r32 + 32ull * k, r);
     const G1A u = g1_to_affine(g1_mul_fr(fp_const(kG1x), fp_const(kG1y), r));
@@ -1233,13 +1287,20 @@ TDEC_KERNEL void tdec_encrypt(uint64_t n, const uint32_t* __restrict__ pk_aff, c
 
 // SecretKeyShare::decrypt_share_no_verify: share = U * sk_i (U already decoded:
 // u_aff records from tdec_pk_prepare over the U48 table).
-TDEC_KERNEL void tdec_decrypt_share(uint64_t n, const uint32_t* __restrict__ u_aff,
+TDEC_KERNEL void tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, const uint32_t* __restrict__ u_aff,
                                     const int32_t* __restrict__ u_status, const uint8_t* __restrict__ sk32,
                                     const uint32_t* __restrict__ share_ct, const uint32_t* __restrict__ share_sk,
-                                    uint8_t* __restrict__ share48, int32_t* __restrict__ status) {
+                                    uint8_t* __restrict__ share48, int32_t* __restrict__ status,
+                                    int32_t* __restrict__ err) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t c = share_ct[k];
+    if (c >= n_ct || share_sk[k] >= n_sk) {  // device-mode index check: identity encoding, HBG_E_ARG
+        g1_compress(share48 + 48ull * k, {fp_zero(), fp_zero(), true});
+        status[k] = HBG_E_ARG;
+        flag_error(err, HBG_E_ARG);
+        return;
+    }
     const uint32_t* ua = u_aff + 32ull * c;
     G1A s = {fp_zero(), fp_zero(), true};
     const int32_t st = u_status[c];
@@ -1391,22 +1452,24 @@ BD G2 g2_mul_ab32(const Fp2& px, const Fp2& py, uint32_t a, uint32_t b) {
     return r;
 }
 
-TDEC_KERNEL void sig_batch_leaves(const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
+TDEC_KERNEL void sig_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t n_doc,
+                                  const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                   const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_pk,
                                   const uint8_t* __restrict__ seeds, const uint32_t* __restrict__ pk_aff,
                                   const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ pk_tbl,
                                   uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= *nb_dev) return;  // grid sized for the bound; the batch count is a device word
     const BatchDesc d = desc[b];
     const uint32_t q = d.start + lane;
     const bool in = q < d.end;
     const uint32_t k = in ? perm[q] : 0u;
     const uint32_t pk = in ? share_pk[k] : 0u;
-    bool valid = in && pk_status[pk] == 0;
+    bool valid = in && pk_status[pk] == 0;  // the sentinel key (out-of-range indices) is invalid
     G2A s;
     if (valid) valid = g2_decompress(share96 + 96ull * k, s, true);
-    if (in) {
+    if (in && d.ct < n_doc) {
         uint8_t m[32 + 96 + 4];
         for (int i = 0; i < 32; ++i) m[i] = seeds[32ull * d.ct + i];
         for (int i = 0; i < 96; ++i) m[32 + i] = share96[96ull * k + i];
@@ -1486,51 +1549,56 @@ BD bool sig_pair_check(const uint32_t* coefH, const Fp& pkx, const Fp& pky, bool
 // batch, or with `spec` over every batch AND its four 16-groups, item
 // 5b + j, so a small batch count does not pay a separate latency-bound round
 // for the 16-groups); lines: one G2Prepared slot per lane of this launch.
-TDEC_KERNEL void sig_batch_check(uint32_t n_items, uint32_t base, uint32_t spec, const CheckItem* __restrict__ items,
+TDEC_KERNEL void sig_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, uint32_t spec,
+                                 const CheckItem* __restrict__ items,
                                  const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                  const uint32_t* __restrict__ sums, const uint8_t* __restrict__ leaf_ok,
                                  const uint32_t* __restrict__ coefH, uint32_t* __restrict__ lines,
                                  uint8_t* __restrict__ ok, CheckItem* __restrict__ next,
                                  uint32_t* __restrict__ next_n, uint32_t* __restrict__ fail_list,
                                  uint32_t* __restrict__ fail_n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_items) return;
-    const uint32_t j = base + i;
+    // items == null: every batch (count *n_dev), or with `spec` every batch and its 16-groups (5 items each)
+    const uint64_t n_items = items ? dev_count(n_dev, cap) : (spec ? 5ull : 1ull) * dev_count(n_dev, cap);
+    uint32_t* my_lines = lines + grid_lane() * kLineWordsPerPoint;  // one G2Prepared slot per resident lane
+    for (uint64_t i = grid_lane(); i < n_items; i += grid_lanes()) {
+    const uint32_t j = (uint32_t)i;
     const CheckItem it = items ? items[j]
                                : (spec ? CheckItem{j / 5u, j % 5u == 0 ? kNodeBatch : kNode16 + j % 5u - 1u}
                                        : CheckItem{j, kNodeBatch});
     const BatchDesc d = desc[it.b];
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
     const uint32_t l0 = node_first(it.node);
-    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;
+    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) continue;
     const uint32_t* sm = sums + (uint64_t)it.b * kSigBatchSumWords + it.node * kSigSumWords;
     const G1A a = g1_to_affine(load_jac(sm));
     const G2A sg = g2_to_affine(load_g2jac(sm + kJacWords));
-    const bool pass = sig_pair_check(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, a.inf, sg,
-                                     lines + (uint64_t)i * kLineWordsPerPoint);
+    const bool pass = sig_pair_check(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, a.inf, sg, my_lines);
     batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n,
                     spec && !items && it.node == kNodeBatch);
+    }
 }
 
 // Per-share PublicKeyShare::verify with H prepared per document: share
 // sel[base + i] (or base + i), lines: one G2Prepared slot per lane.
-TDEC_KERNEL void sig_verify_shares(uint64_t n, uint64_t base, const uint32_t* __restrict__ sel,
+TDEC_KERNEL void sig_verify_shares(uint64_t cap, const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ sel,
                                    const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_doc,
                                    const uint32_t* __restrict__ share_pk, const uint32_t* __restrict__ pk_aff,
                                    const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ coefH,
                                    uint32_t* __restrict__ lines, uint8_t* __restrict__ ok) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t k = sel ? sel[base + i] : base + i;
-    const uint32_t p = share_pk[k];
+    const uint64_t n = dev_count(n_dev, cap);
+    uint32_t* my_lines = lines + grid_lane() * kLineWordsPerPoint;  // one G2Prepared slot per resident lane
+    for (uint64_t i = grid_lane(); i < n; i += grid_lanes()) {
+    const uint64_t k = sel ? sel[i] : i;
+    const uint32_t p = share_pk[k];  // sanitised: an out-of-range pair points at the invalid sentinel key
     G2A sig;
     bool good = pk_status[p] == 0 && g2_decompress(share96 + 96ull * k, sig, true);
     if (good) {
         const uint32_t* pa = pk_aff + 32ull * p;
         good = sig_pair_check(coefH + (uint64_t)share_doc[k] * kLineWordsPerPoint, load_fp(pa), load_fp(pa + 12),
-                              pa[24] != 0, sig, lines + i * kLineWordsPerPoint);
+                              pa[24] != 0, sig, my_lines);
     }
     ok[k] = good ? 1 : 0;
+    }
 }
 
 // ------------------------------------------------------------------ unit-test hook
@@ -1632,13 +1700,30 @@ hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_
     tdec_pk_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, pk48, pk_aff, pk_status);
     return hipGetLastError();
 }
-hipError_t launch_tdec_verify_shares(uint64_t n, const uint8_t* share48, const uint32_t* share_ct,
-                                     const uint32_t* share_pk, const uint32_t* ct_u, const int32_t* ct_status,
-                                     const uint32_t* coefH, const uint32_t* coefW, const uint32_t* pk_aff,
-                                     const int32_t* pk_status, uint8_t* ok, hipStream_t st, const uint32_t* sel) {
+// Grid of a grid-stride round over at most `cap` items: one 64-lane block per
+// 64 items up to the resident limit (2 waves per SIMD on 1,024 SIMDs).
+static dim3 resident_grid(uint64_t cap) {
+    const uint64_t b = (cap + 63) / 64;
+    return dim3((uint32_t)(b < kResidentBlocks ? b : kResidentBlocks));
+}
+
+hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
+                                     const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
+                                     const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
+                                     const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
+                                     const uint32_t* sel) {
+    if (cap == 0) return hipSuccess;
+    tdec_verify_shares<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, share48, share_ct, share_pk, ct_u,
+                                                                ct_status, coefH, coefW, pk_aff, pk_status, ok, sel);
+    return hipGetLastError();
+}
+
+hipError_t launch_tdec_index_sanitize(uint64_t n, const uint32_t* a, uint32_t a_bound, const uint32_t* b,
+                                      uint32_t b_bound, uint32_t* a_out, uint32_t* b_out, int32_t* err,
+                                      hipStream_t st) {
     if (n == 0) return hipSuccess;
-    tdec_verify_shares<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(
-        n, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok, sel);
+    tdec_index_sanitize<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, a, a_bound, b, b_bound, a_out,
+                                                                               b_out, err);
     return hipGetLastError();
 }
 
@@ -1653,13 +1738,14 @@ size_t tdec_batch_temp_bytes(uint32_t n) {
     return (a > b ? (a > c ? a : c) : (b > c ? b : c)) + 256;
 }
 
-// Sort shares by ciphertext (stable), cut batches; bid_n <- number of batches (device word).
-hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* share_ct, uint32_t* keys,
+// Sort shares by ciphertext (stable), cut batches; *nb_dev <- number of batches
+// (a device word: no host round trip).  Keys are < n_keys.
+hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_keys, const uint32_t* share_ct, uint32_t* keys,
                                   uint32_t* perm, uint32_t* tmp_a, uint32_t* tmp_b, BatchDesc* desc, void* temp,
-                                  size_t temp_bytes, uint32_t* nb_out, hipStream_t st) {
+                                  size_t temp_bytes, uint32_t* nb_dev, hipStream_t st) {
     const dim3 g((n + 255) / 256), blk(256);
     int bits = 1;
-    while (bits < 32 && (1ull << bits) < n_ct) ++bits;
+    while (bits < 32 && (1ull << bits) < n_keys) ++bits;
     tdec_iota<<<g, blk, 0, st>>>(n, tmp_a);
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, share_ct, keys, tmp_a, perm, (int)n, 0, bits,
                                                       st);
@@ -1672,19 +1758,24 @@ hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_ct, const uint32_t* sha
     if (e != hipSuccess) return e;
     tdec_batch_desc<<<g, blk, 0, st>>>(n, keys, tmp_a, tmp_b, desc);
     // number of batches = heads in [0, n)
-    e = hipMemcpyAsync(nb_out, tmp_b + (n - 1), 4, hipMemcpyDeviceToHost, st);
-    if (e != hipSuccess) return e;
-    nb_out[1] = 0;
-    return hipStreamSynchronize(st);
+    return hipMemcpyAsync(nb_dev, tmp_b + (n - 1), 4, hipMemcpyDeviceToDevice, st);
 }
 
-hipError_t launch_tdec_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share48,
-                                    const uint32_t* share_pk, const uint8_t* U48, const int32_t* ct_status,
-                                    const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* pk_tbl,
-                                    uint32_t* sums, uint8_t* leaf_ok, hipStream_t st) {
-    if (nb == 0) return hipSuccess;
-    tdec_batch_leaves<<<dim3(nb), dim3(64), 0, st>>>(desc, perm, share48, share_pk, U48, ct_status, pk_aff, pk_status,
-                                                     pk_tbl, sums, leaf_ok);
+uint32_t tdec_batch_bound(uint32_t n, uint32_t n_keys) {
+    // sum over keys of ceil(count / 64) <= n / 64 + (number of distinct keys)
+    const uint64_t distinct = n < n_keys ? n : n_keys;
+    const uint64_t b = (uint64_t)n / kBatchShares + distinct;
+    return (uint32_t)(b < n ? b : n);
+}
+
+hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_ct, const BatchDesc* desc,
+                                    const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
+                                    const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
+                                    const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
+                                    uint8_t* leaf_ok, hipStream_t st) {
+    if (nb_max == 0) return hipSuccess;
+    tdec_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
+                                                         pk_aff, pk_status, pk_tbl, sums, leaf_ok);
     return hipGetLastError();
 }
 
@@ -1696,15 +1787,14 @@ hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t*
     return hipGetLastError();
 }
 
-hipError_t launch_tdec_batch_check(uint32_t n_items, const CheckItem* items, const BatchDesc* desc,
-                                   const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
-                                   const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
-                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
-                                   hipStream_t st) {
-    if (n_items == 0) return hipSuccess;
-    tdec_batch_check<<<dim3((n_items + 63) / 64), dim3(64), 0, st>>>(n_items, items, desc, perm, sums, leaf_ok, ct_u,
-                                                                     coefH, coefW, ok, next, next_n, fail_list,
-                                                                     fail_n);
+hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const CheckItem* items,
+                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
+                                   const uint8_t* leaf_ok, const uint32_t* ct_u, const uint32_t* coefH,
+                                   const uint32_t* coefW, uint8_t* ok, CheckItem* next, uint32_t* next_n,
+                                   uint32_t* fail_list, uint32_t* fail_n, hipStream_t st) {
+    if (cap == 0) return hipSuccess;
+    tdec_batch_check<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, items, desc, perm, sums, leaf_ok, ct_u,
+                                                              coefH, coefW, ok, next, next_n, fail_list, fail_n);
     return hipGetLastError();
 }
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
@@ -1723,17 +1813,17 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
     return hipGetLastError();
 }
 static dim3 grid64(uint64_t n) { return dim3((uint32_t)((n + 63) / 64)); }
-hipError_t launch_bls_sign(uint64_t n, const uint8_t* sk32, const uint32_t* msg_sk, const uint8_t* msg,
-                           const uint64_t* off, uint8_t* sig96, hipStream_t st) {
+hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
+                           const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    bls_sign<<<grid64(n), dim3(64), 0, st>>>(n, sk32, msg_sk, msg, off, sig96);
+    bls_sign<<<grid64(n), dim3(64), 0, st>>>(n, n_sk, sk32, msg_sk, msg, off, sig96, err);
     return hipGetLastError();
 }
-hipError_t launch_bls_verify(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint32_t* msg_pk,
-                             const uint8_t* msg, const uint64_t* off, const uint8_t* sig96, uint32_t* lines,
-                             uint8_t* ok, hipStream_t st) {
+hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
+                             const uint32_t* msg_pk, const uint8_t* msg, const uint64_t* off, const uint8_t* sig96,
+                             uint32_t* lines, uint8_t* ok, int32_t* err, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    bls_verify<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok);
+    bls_verify<<<grid64(n), dim3(64), 0, st>>>(n, n_pk, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok, err);
     return hipGetLastError();
 }
 hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
@@ -1744,17 +1834,20 @@ hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const i
                                                        status);
     return hipGetLastError();
 }
-hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const uint8_t* r32, const uint8_t* msg,
-                               const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96, hipStream_t st) {
+hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
+                               const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
+                               int32_t* err, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    tdec_encrypt<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, r32, msg, off, U48, V, W96);
+    tdec_encrypt<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, r32, msg, off, U48, V, W96, err);
     return hipGetLastError();
 }
-hipError_t launch_tdec_decrypt_share(uint64_t n, const uint32_t* u_aff, const int32_t* u_status, const uint8_t* sk32,
-                                     const uint32_t* share_ct, const uint32_t* share_sk, uint8_t* share48,
-                                     int32_t* status, hipStream_t st) {
+hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, const uint32_t* u_aff,
+                                     const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
+                                     const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
+                                     hipStream_t st) {
     if (n == 0) return hipSuccess;
-    tdec_decrypt_share<<<grid64(n), dim3(64), 0, st>>>(n, u_aff, u_status, sk32, share_ct, share_sk, share48, status);
+    tdec_decrypt_share<<<grid64(n), dim3(64), 0, st>>>(n, n_ct, n_sk, u_aff, u_status, sk32, share_ct, share_sk,
+                                                       share48, status, err);
     return hipGetLastError();
 }
 hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, const uint32_t* idx, uint8_t* sig96,
@@ -1778,35 +1871,34 @@ hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t
     sig_doc_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, doc, off, coefH, seeds);
     return hipGetLastError();
 }
-hipError_t launch_sig_batch_leaves(uint32_t nb, const BatchDesc* desc, const uint32_t* perm, const uint8_t* share96,
-                                   const uint32_t* share_pk, const uint8_t* seeds, const uint32_t* pk_aff,
-                                   const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
-                                   uint8_t* leaf_ok, hipStream_t st) {
-    if (nb == 0) return hipSuccess;
-    sig_batch_leaves<<<dim3(nb), dim3(64), 0, st>>>(desc, perm, share96, share_pk, seeds, pk_aff, pk_status, pk_tbl,
-                                                    sums, leaf_ok);
+hipError_t launch_sig_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_doc, const BatchDesc* desc,
+                                   const uint32_t* perm, const uint8_t* share96, const uint32_t* share_pk,
+                                   const uint8_t* seeds, const uint32_t* pk_aff, const int32_t* pk_status,
+                                   const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, hipStream_t st) {
+    if (nb_max == 0) return hipSuccess;
+    sig_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_dev, n_doc, desc, perm, share96, share_pk, seeds, pk_aff,
+                                                        pk_status, pk_tbl, sums, leaf_ok);
     return hipGetLastError();
 }
-hipError_t launch_sig_batch_check(uint32_t n_items, uint32_t base, uint32_t spec, const CheckItem* items,
+// lines: kResidentBlocks * 64 G2Prepared slots (one per resident lane)
+hipError_t launch_sig_batch_check(uint32_t cap, const uint32_t* n_dev, uint32_t spec, const CheckItem* items,
                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
                                   const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
                                   hipStream_t st) {
-    if (n_items == 0) return hipSuccess;
-    sig_batch_check<<<dim3((n_items + 63) / 64), dim3(64), 0, st>>>(n_items, base, spec, items, desc, perm, sums,
-                                                                    leaf_ok,
-                                                                    coefH, lines, ok, next, next_n, fail_list,
-                                                                    fail_n);
+    if (cap == 0) return hipSuccess;
+    const uint64_t items_cap = items ? cap : (spec ? 5ull : 1ull) * cap;
+    sig_batch_check<<<resident_grid(items_cap), dim3(64), 0, st>>>(cap, n_dev, spec, items, desc, perm, sums, leaf_ok,
+                                                                   coefH, lines, ok, next, next_n, fail_list, fail_n);
     return hipGetLastError();
 }
-hipError_t launch_sig_verify_shares(uint64_t n, uint64_t base, const uint32_t* sel, const uint8_t* share96,
+hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint32_t* sel, const uint8_t* share96,
                                     const uint32_t* share_doc, const uint32_t* share_pk, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
                                     hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    sig_verify_shares<<<dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st>>>(n, base, sel, share96, share_doc,
-                                                                            share_pk, pk_aff, pk_status, coefH,
-                                                                            lines, ok);
+    if (cap == 0) return hipSuccess;
+    sig_verify_shares<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, sel, share96, share_doc, share_pk, pk_aff,
+                                                               pk_status, coefH, lines, ok);
     return hipGetLastError();
 }
 

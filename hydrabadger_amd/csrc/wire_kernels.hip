@@ -98,16 +98,18 @@ __global__ __launch_bounds__(256) void rbc_write_proof_msgs(uint32_t N, uint64_t
                                                             const uint32_t* __restrict__ index,
                                                             uint8_t* __restrict__ out,
                                                             const uint64_t* __restrict__ out_off,
-                                                            uint32_t blocks_per_msg) {
+                                                            uint32_t blocks_per_msg, int32_t* __restrict__ err) {
     const uint64_t j = blockIdx.x / blocks_per_msg;
     if (j >= m) return;
     const uint32_t i = index[j];
-    if (i >= N) return;
+    const uint64_t ki = inst[j];
     const uint32_t k = proof_digests(N, i);
     const uint64_t start = out_off[j], end = out_off[j + 1];
-    if (end - start != 12 + L + 16 + 32ull * k + 32) return;  // layout mismatch: host mode rejects it up front
-    const uint64_t ki = inst[j];
-    if (ki >= n) return;
+    // device-mode argument check (host mode rejects these up front): the message stays unwritten
+    if (i >= N || ki >= n || end < start || end - start != 12 + L + 16 + 32ull * k + 32) {
+        if (blockIdx.x % blocks_per_msg == 0 && threadIdx.x == 0) flag_error(err, HBG_E_ARG);
+        return;
+    }
     const uint8_t* row = shards + (ki * N + i) * S;
     const uint8_t* lev = levels + ki * nodes * 32ull;
     const uint64_t c0 = (uint64_t)(blockIdx.x % blocks_per_msg) * 256 * kChunks + threadIdx.x;
@@ -229,24 +231,28 @@ __global__ __launch_bounds__(256) void rbc_read_msgs(uint64_t L, const uint8_t* 
 }
 
 // WireMessages::start_send framing: u32 BE (8 + len + 96) | u64 LE len |
-// message | sig96 (sig from bls_sign into a [n][96] table).  grid: n frames x
-// blocks_per_frame; thread = one 16-B destination chunk, as above.
+// message | sig96 (sig from bls_sign into a [n][96] table).  One 256-thread
+// block per frame, thread = one 16-B destination chunk per pass (frames are
+// sized from the device offsets: no host round trip in device mode).  A frame
+// whose slot size is wrong, or whose body exceeds the codec's 8 MiB limit,
+// stays unwritten and flags HBG_E_ARG / HBG_E_WIRE_FRAME.
 __global__ __launch_bounds__(256) void wire_frame_pack(uint64_t n, const uint8_t* __restrict__ msg,
                                                        const uint64_t* __restrict__ msg_off,
                                                        const uint8_t* __restrict__ sig96, uint8_t* __restrict__ frames,
                                                        const uint64_t* __restrict__ frame_off,
-                                                       uint32_t blocks_per_frame) {
-    const uint64_t k = blockIdx.x / blocks_per_frame;
+                                                       int32_t* __restrict__ err) {
+    const uint64_t k = blockIdx.x;
     if (k >= n) return;
     const uint64_t len = msg_off[k + 1] - msg_off[k];
     const uint64_t start = frame_off[k], end = frame_off[k + 1];
-    if (end - start != 12 + len + 96) return;
-    const uint8_t* m = msg + msg_off[k];
     const uint64_t body = 8 + len + 96;
-    const uint64_t c0 = (uint64_t)(blockIdx.x % blocks_per_frame) * 256 * kChunks + threadIdx.x;
-#pragma unroll
-    for (uint32_t q = 0; q < kChunks; ++q) {
-        const uint64_t A = (start & ~15ull) + 16 * (c0 + 256 * q);
+    if (msg_off[k + 1] < msg_off[k] || end < start || end - start != 12 + len + 96 || body > (uint64_t)HBG_WIRE_MAX_FRAME) {
+        if (threadIdx.x == 0) flag_error(err, body > (uint64_t)HBG_WIRE_MAX_FRAME ? HBG_E_WIRE_FRAME : HBG_E_ARG);
+        return;
+    }
+    const uint8_t* m = msg + msg_off[k];
+    for (uint64_t c = threadIdx.x;; c += 256) {
+        const uint64_t A = (start & ~15ull) + 16 * c;
         if (A >= end) return;
         if (A >= start + 12 && A + 16 <= start + 12 + len) {
             *reinterpret_cast<uint4*>(frames + A) = load16_unaligned(m + (A - start - 12));
@@ -266,24 +272,22 @@ __global__ __launch_bounds__(256) void wire_frame_pack(uint64_t n, const uint8_t
 }
 
 hipError_t launch_wire_frame_pack(uint64_t n, const uint8_t* msg, const uint64_t* msg_off, const uint8_t* sig96,
-                                  uint8_t* frames, const uint64_t* frame_off, uint64_t max_len, hipStream_t st) {
+                                  uint8_t* frames, const uint64_t* frame_off, int32_t* err, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    const uint64_t bpf64 = ((12 + max_len + 96) + 32 + kBlockBytes - 1) / kBlockBytes;
-    const uint32_t bpf = (uint32_t)bpf64;
-    hipLaunchKernelGGL(wire_frame_pack, dim3((uint32_t)(n * bpf)), dim3(256), 0, st, n, msg, msg_off, sig96, frames,
-                       frame_off, bpf);
+    hipLaunchKernelGGL(wire_frame_pack, dim3((uint32_t)n), dim3(256), 0, st, n, msg, msg_off, sig96, frames, frame_off,
+                       err);
     return hipGetLastError();
 }
 
 hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* shards, uint64_t S,
                                        const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m,
                                        const uint64_t* inst, const uint32_t* index, uint8_t* out,
-                                       const uint64_t* out_off, hipStream_t st) {
+                                       const uint64_t* out_off, int32_t* err, hipStream_t st) {
     if (m == 0) return hipSuccess;
     const uint64_t max_len = 12 + L + 16 + 32ull * merkle_depth(N) + 32;
     const uint32_t bpm = (uint32_t)((max_len + 32 + kBlockBytes - 1) / kBlockBytes);
     hipLaunchKernelGGL(rbc_write_proof_msgs, dim3((uint32_t)(m * bpm)), dim3(256), 0, st, N, L, shards, S, levels,
-                       merkle_nodes(N), n, tag, m, inst, index, out, out_off, bpm);
+                       merkle_nodes(N), n, tag, m, inst, index, out, out_off, bpm, err);
     return hipGetLastError();
 }
 

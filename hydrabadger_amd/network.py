@@ -73,13 +73,25 @@ def arrival_mask(instance: int, n: int, epoch: int = 0) -> list:
 
 class DeviceEngine:
     """The product engine: libhbgpu.so kernels on this rank's GPU (torch CUDA
-    tensors as device buffers, the context bound to the current stream)."""
+    tensors as device buffers).
+
+    Every torch op here (zero fills, gathers, the arrival mask) runs on torch's
+    current stream and the engine's kernels read what they produce, so the
+    context must enqueue on that same stream: a context created here is bound
+    to ``torch.cuda.current_stream(device)``; a context passed in must already
+    be bound to the stream the caller runs torch on (bench.py binds its own).
+    One stream also makes the caching allocator's reuse of tensors freed while
+    an HBG_ASYNC kernel still reads them safe (reuse is ordered on the stream).
+    """
 
     def __init__(self, device: torch.device, ctx: _lib.Context | None = None):
         if device.type != "cuda":
             raise _lib.HbgError(_lib.HBG_E_DEVICE, "DeviceEngine needs a GPU (no CPU fallback)")
         self.device = device
-        self.ctx = ctx or _lib.Context(device.index if device.index is not None else 0)
+        if ctx is None:
+            ctx = _lib.Context(device.index if device.index is not None else 0)
+            ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        self.ctx = ctx
 
     def zeros(self, shape, dtype=torch.uint8):
         return torch.zeros(shape, dtype=dtype, device=self.device)

@@ -15,7 +15,16 @@
  *    arrays) is a device pointer on the context's device; otherwise all are
  *    host pointers and the engine stages them through device memory.
  *  - flags & HBG_ASYNC (device mode only): return after enqueueing on the
- *    context stream; call hbg_sync().  Without it calls are synchronous.
+ *    context stream, with no host synchronisation inside the call (only the
+ *    one-time growth of an internal scratch buffer waits for the stream);
+ *    call hbg_sync().  Without it calls are synchronous.
+ *  - Device-side argument errors: in device mode the index / length
+ *    arguments live in device memory, so the kernels check them.  An
+ *    offending item gets its invalid per-item output (ok = 0, status =
+ *    HBG_E_ARG, an all-zero point encoding, a message or frame left
+ *    unwritten) and the context records the FIRST such code; the next
+ *    synchronous call or hbg_sync() returns it (and clears it).  Host mode
+ *    rejects the same arguments up front with the same code.
  *  - Shard batches: instance k's shard i starts at
  *        shards + (k * N + i) * shard_stride
  *    and holds shard_len (L) meaningful bytes.  Host mode accepts any
@@ -125,8 +134,10 @@ int hbg_merkle_validate(hbg_ctx *ctx, uint32_t N, uint64_t value_len, const uint
 /* Broadcast::send_shards fused (a2+a3+a4): payload k (payload_len[k] bytes at
  * payloads + k*payload_stride) -> BE u32 length prefix, zero pad, chunk into N
  * shards of shard_len, RS-encode, Merkle-tree.  Every payload_len[k] must give
- * hbg_shard_len(N, payload_len[k]) == shard_len (else HBG_E_ARG).  Device mode
- * additionally needs payload_stride % 4 == 0. */
+ * hbg_shard_len(N, payload_len[k]) == shard_len and payload_len[k] <=
+ * payload_stride (else HBG_E_ARG; in device mode such an instance is skipped
+ * and the error is device-side).  Device mode additionally needs
+ * payload_stride % 4 == 0. */
 int hbg_rbc_encode_merkle(hbg_ctx *ctx, uint32_t N, const uint8_t *payloads,
                           uint64_t payload_stride, const uint64_t *payload_len,
                           uint64_t shard_len, uint8_t *shards, uint64_t shard_stride,
@@ -153,7 +164,8 @@ int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards
  * key share pk48[share_pk[k]] (PublicKeySet::public_key_share(i) values).
  * ok[k] = 1 iff every point decodes (in its subgroup), the ciphertext decodes,
  * and e(share, hash_g1_g2(U, V)) == e(pk, W).  Bit-identical to the crate's
- * bool for points the crate would deserialise. */
+ * bool for points the crate would deserialise.  share_ct[k] >= n_ct or
+ * share_pk[k] >= n_pk: HBG_E_ARG (device mode: ok[k] = 0, device-side). */
 int hbg_tdec_verify_shares(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, const uint8_t *V,
                            const uint64_t *V_off, const uint8_t *W96, uint32_t n_pk,
                            const uint8_t *pk48, uint64_t n_shares, const uint8_t *share48,
@@ -183,7 +195,8 @@ int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *sha
 /* PublicKey::encrypt_with_rng (threshold_crypto) with the randomness explicit:
  * for message k (msg[msg_off[k] .. msg_off[k+1]]) and scalar r32[k]:
  * U48[k] = r G1, V (at the message's offsets) = xor_with_hash(r PK, msg),
- * W96[k] = r hash_g1_g2(U, V).  HBG_E_INVALID_POINT if pk48 does not decode.
+ * W96[k] = r hash_g1_g2(U, V).  HBG_E_INVALID_POINT if pk48 does not decode
+ * (device-side: U48 / W96 are then all-zero).
  * Replaces the reference call inside hbbft HoneyBadger::propose
  * (reached from src/hydrabadger/state.rs:484). */
 int hbg_tdec_encrypt(hbg_ctx *ctx, const uint8_t *pk48, uint64_t n, const uint8_t *r32,
@@ -193,7 +206,8 @@ int hbg_tdec_encrypt(hbg_ctx *ctx, const uint8_t *pk48, uint64_t n, const uint8_
 /* SecretKeyShare::decrypt_share_no_verify for n (ciphertext, key) pairs:
  * share48[k] = U48[share_ct[k]] * sk32[share_sk[k]].  status[k] = 0, or
  * HBG_E_INVALID_POINT when that U does not decode (share48[k] is then the
- * identity encoding).  Reached from hbbft ThresholdDecrypt::start_decryption
+ * identity encoding), or HBG_E_ARG for an out-of-range index (device mode).
+ * Reached from hbbft ThresholdDecrypt::start_decryption
  * (src/hydrabadger/state.rs:487). */
 int hbg_tdec_decrypt_shares(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, uint32_t n_sk,
                             const uint8_t *sk32, uint64_t n, const uint32_t *share_ct,
@@ -202,7 +216,8 @@ int hbg_tdec_decrypt_shares(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, uin
 
 /* ---- wire-message signatures --------------------------
  * SecretKey::sign(msg) for n messages: sig96[k] = hash_g2(msg_k) * sk32[msg_sk[k]]
- * (replaces src/lib.rs:434, WireMessages::start_send). */
+ * (replaces src/lib.rs:434, WireMessages::start_send).  msg_sk[k] >= n_sk:
+ * HBG_E_ARG (device mode: sig96[k] all-zero, device-side). */
 int hbg_bls_sign(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint64_t n,
                  const uint32_t *msg_sk, const uint8_t *msg, const uint64_t *msg_off,
                  uint8_t *sig96, uint32_t flags);
@@ -210,7 +225,8 @@ int hbg_bls_sign(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint64_t n,
 /* PublicKey::verify(sig, msg) for n messages: ok[k] = 1 iff pk48[msg_pk[k]]
  * and sig96[k] decode (the crate's subgroup checks) and
  * e(pk, hash_g2(msg_k)) == e(G1, sig) (replaces src/lib.rs:405-416,
- * WireMessages::poll). */
+ * WireMessages::poll).  msg_pk[k] >= n_pk: HBG_E_ARG (device mode: ok[k] = 0,
+ * device-side). */
 int hbg_bls_verify(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
                    const uint32_t *msg_pk, const uint8_t *msg, const uint64_t *msg_off,
                    const uint8_t *sig96, uint8_t *ok, uint32_t flags);
@@ -236,8 +252,9 @@ int hbg_sig_combine(hbg_ctx *ctx, uint32_t t, uint64_t n, const uint8_t *share96
  * same (pk, doc, share): 1 iff the key and the share decode (subgroup checks)
  * and e(pk, hash_g2(doc)) == e(G1, share).  hash_g2 runs once per document
  * and shares of one document are checked in weighted batches (a failing
- * batch falls back to the per-share equation); HBG_TDEC_BATCHED=0 /
- * hbg_test_set_tdec_batched(ctx, 0) select the per-share schedule.  Replaces
+ * batch falls back to the per-share equation); hbg_test_set_tdec_batched(ctx, 0)
+ * selects the per-share schedule.  Out-of-range indices as in
+ * hbg_tdec_verify_shares.  Replaces
  * hbbft ThresholdSign::handle_message's PublicKeyShare::verify (reached from
  * src/hydrabadger/state.rs:487). */
 int hbg_sig_verify_shares(hbg_ctx *ctx, uint32_t n_doc, const uint8_t *doc, const uint64_t *doc_off,
@@ -270,8 +287,9 @@ uint64_t hbg_proof_msg_len(uint32_t N, uint32_t index, uint64_t value_len); /* b
  * j < m, from a shard batch of n instances (the hbg_rbc_encode_merkle /
  * hbg_merkle_build layout: shards, shard_stride, levels).  Message j is
  * written to out[out_off[j] .. out_off[j+1]), which must be exactly
- * hbg_proof_msg_len(N, index[j], shard_len) bytes (HBG_E_ARG otherwise in
- * host mode; device mode leaves such a message unwritten).  tag is
+ * hbg_proof_msg_len(N, index[j], shard_len) bytes, with index[j] < N and
+ * inst[j] < n (HBG_E_ARG otherwise; device mode leaves such a message
+ * unwritten and the error is device-side).  tag is
  * HBG_MSG_VALUE or HBG_MSG_ECHO.  Device mode needs shard_stride % 16 == 0 and
  * 16-byte-aligned shards and out. */
 int hbg_rbc_write_proof_msgs(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, const uint8_t *shards,
@@ -306,6 +324,11 @@ int hbg_rbc_read_msgs(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, const uint8_
 #define HBG_WIRE_KIND_MESSAGE 7u
 #define HBG_WIRE_KIND_KEYGEN 9u
 #define HBG_WIRE_KIND_MAX 10u
+/* LengthDelimitedCodec::new()'s default max_frame_length (tokio-io 0.1,
+ * src/lib.rs:369): a frame body (= 8 + len + 96) above it is an error on both
+ * sides — HBG_E_WIRE_FRAME from hbg_wire_verify_frames, and
+ * hbg_wire_sign_frames refuses it (HBG_E_WIRE_FRAME). */
+#define HBG_WIRE_MAX_FRAME (8u * 1024u * 1024u)
 
 uint64_t hbg_wire_frame_len(uint64_t msg_len); /* 4 + 8 + msg_len + 96 */
 
@@ -313,8 +336,9 @@ uint64_t hbg_wire_frame_len(uint64_t msg_len); /* 4 + 8 + msg_len + 96 */
  * (msg[msg_off[k] .. msg_off[k+1]]) signed with sk32[msg_sk[k]]
  * (SecretKey::sign, src/lib.rs:434) and framed into
  * frames[frame_off[k] .. frame_off[k+1]] (exactly hbg_wire_frame_len bytes:
- * HBG_E_ARG otherwise in host mode; device mode leaves such a frame
- * unwritten). */
+ * HBG_E_ARG otherwise; a body over HBG_WIRE_MAX_FRAME: HBG_E_WIRE_FRAME, as
+ * FramedWrite refuses it; device mode leaves such a frame unwritten and the
+ * error is device-side). */
 int hbg_wire_sign_frames(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint64_t n,
                          const uint32_t *msg_sk, const uint8_t *msg, const uint64_t *msg_off,
                          uint8_t *frames, const uint64_t *frame_off, uint32_t flags);
@@ -326,8 +350,12 @@ int hbg_wire_sign_frames(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint6
  * kind the reference does not verify), HBG_E_WIRE_FRAME, HBG_E_WIRE_EOF,
  * HBG_E_INVALID_POINT (sig does not deserialise), HBG_E_WIRE_TAG (kind > 10),
  * HBG_E_UNKNOWN_PEER or HBG_E_INVALID_SIGNATURE.  The message of frame k is
- * frames[frame_off[k] + 12 ..][..len].  Beyond the kind index the inner
- * WireMessage is not deserialised (control plane). */
+ * frames[frame_off[k] + 12 ..][..len].  status 0 covers the frame (codec
+ * prefix, HBG_WIRE_MAX_FRAME), the SignedWireMessage layout, the signature
+ * point and the WireMessageKind index only: poll's bincode deserialisation
+ * of the rest of the WireMessage body (src/lib.rs:402-403, Error::Serde on
+ * a malformed body) is left to the caller, which must still deserialise
+ * the message it dispatches (control plane). */
 int hbg_wire_verify_frames(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
                            const uint32_t *frame_pk, const uint8_t *frames, const uint64_t *frame_off,
                            int32_t *status, uint32_t flags);

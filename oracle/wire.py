@@ -104,6 +104,9 @@ def deserialize(msg: bytes):
 # Signature serialises as its 96-byte compressed G2 point, a serde tuple
 # (threshold_crypto serde_impl::projective) — no length; parity unpinned.
 KIND_MESSAGE, KIND_KEYGEN, KIND_MAX = 7, 9, 10
+# LengthDelimitedCodec::new() (tokio-io 0.1, src/lib.rs:369): default
+# max_frame_length 8 MiB; a longer frame is an error on read and on write.
+MAX_FRAME = 8 * 1024 * 1024
 E_WIRE_FRAME = -32
 E_INVALID_SIGNATURE = -33
 E_UNKNOWN_PEER = -34
@@ -128,7 +131,8 @@ def poll_frame(frame: bytes, peer_pk=None) -> int:
     frame = bytes(frame)
     if len(frame) < 4:
         return E_WIRE_EOF
-    if struct.unpack_from(">I", frame, 0)[0] != len(frame) - 4:
+    head = struct.unpack_from(">I", frame, 0)[0]
+    if head > MAX_FRAME or head != len(frame) - 4:  # codec: frame too big / not one whole frame
         return E_WIRE_FRAME
     if len(frame) < 12:
         return E_WIRE_EOF
