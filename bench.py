@@ -59,6 +59,9 @@ def merkle_alg(N: int, L: int):
     return ops, bytes_
 
 
+LEGS = ("rbc", "decode", "bwire", "epoch", "tdec", "wire", "f1", "coin")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,6 +83,8 @@ def parse():
                     help="SURVEY.md §8(f4): instances whose N Value messages are written/parsed/validated (0 disables)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--legs", default="all",
+                    help="comma list of legs besides the timed step: " + ",".join(LEGS) + " (default all)")
     return ap.parse_args()
 
 
@@ -128,112 +133,163 @@ def cpu_baseline(n_sample: int):
             "simd": bool(corc.lib().orc_simd_enabled())}
 
 
-def _tdec_fixture():
-    # N=64 t=21 key material (BASELINE.json configs[3]): 4 ciphertexts x 64 shares, made
-    # by tests/golden/make_golden_tdec.py.  Threshold material cannot be generated on the
-    # device yet (encrypt_with_rng is SURVEY.md §8(f1)); the fixture is replicated.
-    return json.load(open(os.path.join(ROOT, "tests", "golden", "tdec_n64.json")))["scenario"]
+# TDec roofline constants.  Every Fp multiplication / squaring the kernels run
+# is a generated 12x12-limb Montgomery CIOS body of 288 v_mad_u64_u32
+# (tools/gen_bls_fp.py; counted in the gfx950 asm).  The peak is the measured
+# v_mad_u64_u32 issue rate — 4.44 cycles per wave-instruction per SIMD at 8
+# waves/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) — at the 2.4 GHz
+# nominal clock on 1,024 SIMDs: 35.4 T lane-MADs/s.
+MADS_PER_FP_MUL = 288
+MAD_PEAK = 256 * 4 * 64 / 4.44 * 2.4e9
 
 
-def cpu_baseline_tdec(n_ct: int = 64, n_comb: int = 256):
+def fp_count_profile(n_nodes: int, t: int, bad_rate: float) -> dict:
+    """Per-share Fp-multiplication counts of the ThresholdDecrypt driver's
+    kernels, measured by the instrumented build (tools/fpcount.py ->
+    profiles/fpcount.json) on the same generator at a smaller ciphertext
+    count; empty when the committed profile is for another shape."""
+    path = os.path.join(ROOT, "profiles", "fpcount.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    sh = d.get("shape", {})
+    if (sh.get("n_nodes"), sh.get("t"), sh.get("bad_rate")) != (n_nodes, t, bad_rate):
+        return {}
+    d["path"] = os.path.relpath(path, ROOT)
+    return d
+
+
+def kernel_meta(names) -> dict:
+    """VGPR / scratch / waves-per-SIMD of the named kernels (tools/kernel_meta.py)."""
+    try:
+        k = json.load(open(os.path.join(ROOT, "profiles", "kernel_meta.json")))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return {}
+    out = {}
+    for mangled, v in k.items():
+        for n in names:
+            if f"{len(n)}{n}E" in mangled:
+                out[n] = {x: v[x] for x in ("vgpr", "agpr", "sgpr", "scratch_bytes", "lds_bytes",
+                                            "waves_per_simd_by_regs")}
+    return out
+
+
+def cpu_baseline_tdec(ep, n_ct: int = 64):
     """The C restatement of threshold_crypto's per-share algorithm
     (oracle/c/bls_oracle.c: share decode with the crate's [r]P subgroup check,
-    hash_g1_g2 recomputed per call, two full pairings), ciphertexts and key
-    shares decoded once; one contiguous block of shares per host thread."""
+    hash_g1_g2 recomputed per call, two full pairings per
+    verify_decryption_share) on the first n_ct ciphertexts of the SAME
+    device-generated epoch the GPU leg runs: verify all N shares of each,
+    then PublicKeySet::decrypt of the first t+1 valid ones (node order), one
+    contiguous block of shares per host thread."""
+    from hydrabadger_amd import tdec_workload as tw
     from oracle import corb
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
     threads = max(1, min(threads, os.cpu_count() or 1, 64))
-    g = _tdec_fixture()
-    K, n, t = len(g["cts"]), len(g["pk_shares"]), g["t"]
-    base = [(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in g["cts"]]
-    cts = [base[j % K] for j in range(max(n_ct, n_comb))]
-    U, V, off, W = corb._ct_table(cts[:n_ct])
-    pk = np.frombuffer(b"".join(bytes.fromhex(p) for p in g["pk_shares"]), np.uint8).copy()
-    sh = np.frombuffer(b"".join(bytes.fromhex(g["cts"][j % K]["shares"][i]) for j in range(n_ct) for i in range(n)),
-                       np.uint8).copy()
-    sct = np.repeat(np.arange(n_ct, dtype=np.uint32), n)
-    spk = np.tile(np.arange(n, dtype=np.uint32), n_ct)
+    N, t, L = ep.n_nodes, ep.t, ep.msg_len
+    U = ep.U[:n_ct].cpu().numpy().reshape(-1).copy()
+    W = ep.W[:n_ct].cpu().numpy().reshape(-1).copy()
+    V = np.concatenate([ep.V[:n_ct * L].cpu().numpy(), np.zeros(1, np.uint8)])
+    off = (np.arange(n_ct + 1, dtype=np.uint64) * L)
+    pk = ep.pk48.cpu().numpy().reshape(-1).copy()
+    sh = ep.share48[:n_ct].cpu().numpy().reshape(-1).copy()
+    sct = np.repeat(np.arange(n_ct, dtype=np.uint32), N)
+    spk = np.tile(np.arange(N, dtype=np.uint32), n_ct)
     t0 = time.perf_counter()
     ok = corb.verify_shares_arrays(threads, U, V, off, W, pk, sh, sct, spk)
     tv = time.perf_counter() - t0
-    _, Vc, offc, _ = corb._ct_table(cts[:n_comb])
-    csh = np.frombuffer(b"".join(bytes.fromhex(g["cts"][j % K]["shares"][i]) for j in range(n_comb)
-                                 for i in range(t + 1)), np.uint8).copy()
-    ix = np.tile(np.arange(t + 1, dtype=np.uint32), n_comb)
+    acc = tw.expected_outcomes(ep.bad[:n_ct], t) == 1
+    ix = np.stack([np.nonzero(acc[k])[0][: t + 1] for k in range(n_ct)]).astype(np.uint32)
+    csh = ep.share48[:n_ct].cpu().numpy()[np.arange(n_ct)[:, None], ix].reshape(-1).copy()
     t0 = time.perf_counter()
-    out, st = corb.decrypt_arrays(threads, t, csh, ix, Vc, offc)
+    out, st = corb.decrypt_arrays(threads, t, csh, ix.reshape(-1).copy(), V, off)
     tc = time.perf_counter() - t0
-    ref = b"".join(bytes.fromhex(g["cts"][j % K]["plaintext"]) for j in range(n_comb))
-    return {"value": n_ct * n / tv, "unit": "shares/s", "cores": threads, "kind": "port",
-            "combine_cts_per_s": n_comb / tc,
-            "sample": f"{n_ct * n} verify_decryption_share ({n_ct} ciphertexts x {n}) in {tv:.2f} s + {n_comb} "
-                      f"PublicKeySet::decrypt (t={t}) in {tc:.2f} s, oracle/c/bls_oracle.c -O3 (64-bit limbs, "
-                      f"the crate's per-share algorithm), {threads} threads",
-            "all_valid": bool(ok.all()) and bool((st == 0).all()) and out[:len(ref)].tobytes() == ref}
+    ref = ep.msgs[:n_ct * L].cpu().numpy().tobytes()
+    return {"value": n_ct * N / (tv + tc), "unit": "shares/s", "cores": threads, "kind": "port",
+            "verify_shares_per_s": n_ct * N / tv, "combine_cts_per_s": n_ct / tc,
+            "sample": f"{n_ct} ciphertexts x {N} shares of the bench's device-generated epoch: {n_ct * N} "
+                      f"verify_decryption_share in {tv:.2f} s + {n_ct} PublicKeySet::decrypt (t={t}) in {tc:.2f} s, "
+                      f"oracle/c/bls_oracle.c -O3 (64-bit limbs, the crate's per-share algorithm), {threads} threads",
+            "bits_match": bool(np.array_equal(ok.astype(bool), ~ep.bad[:n_ct].reshape(-1))),
+            "plaintexts_match": bool((st == 0).all()) and out[:len(ref)].tobytes() == ref}
 
 
-def tdec_leg(ctx, dev, n_ct: int, reps: int):
-    """Verify all 64 shares of n_ct ciphertexts (1 % corrupted) + combine the first
-    t+1 valid shares of each: hbg_tdec_verify_shares + hbg_tdec_combine on
-    device-resident inputs."""
+def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.01):
+    """BASELINE.json configs[3]: one node's ThresholdDecrypt for an epoch of
+    n_ct DISTINCT ciphertexts (N=64, t=21), device-generated
+    (hydrabadger_amd/tdec_workload.py: encrypt_with_rng + every node's
+    decrypt_share_no_verify, 1 % of the shares replaced by three kinds of bad
+    share), through hbg_tdec_threshold_decrypt: Ciphertext::verify, all 64
+    shares verified, first t+1 valid selected (faults / ignored late shares),
+    PublicKeySet::decrypt.  Inputs HBM-resident; the verify call alone is
+    timed beside it."""
     from hydrabadger_amd import _lib
-    g = _tdec_fixture()
-    K, n, t = len(g["cts"]), len(g["pk_shares"]), g["t"]
-    base = [(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in g["cts"]]
-    U = np.frombuffer(b"".join(base[j % K][0] for j in range(n_ct)), np.uint8)
-    W = np.frombuffer(b"".join(base[j % K][2] for j in range(n_ct)), np.uint8)
-    Vb = b"".join(base[j % K][1] for j in range(n_ct))
-    off = np.zeros(n_ct + 1, np.uint64)
-    off[1:] = np.cumsum([len(base[j % K][1]) for j in range(n_ct)])
-    pk = np.frombuffer(b"".join(bytes.fromhex(p) for p in g["pk_shares"]), np.uint8)
-    sh_base = np.array([[np.frombuffer(bytes.fromhex(x), np.uint8) for x in c["shares"]] for c in g["cts"]])
-    ct_of = np.arange(n_ct) % K
-    share = np.ascontiguousarray(sh_base[ct_of]).reshape(-1)          # [n_ct][n][48]
-    sct = np.repeat(np.arange(n_ct, dtype=np.uint32), n)
-    spk = np.tile(np.arange(n, dtype=np.uint32), n_ct)
-    rng = np.random.default_rng(0x48424247)
-    bad = rng.random(n_ct * n) < 0.01          # seeded 1 % corrupted: claimed under the wrong key
-    spk[bad] = (spk[bad] + 1) % n
-    expect = (~bad).astype(np.uint8)
-    # combine the first t+1 valid shares of each ciphertext, in index order
-    ix = np.argsort(bad.reshape(n_ct, n), axis=1, kind="stable")[:, : t + 1].astype(np.uint32)
-    assert not bad.reshape(n_ct, n)[np.arange(n_ct)[:, None], ix].any()
-    csh = np.ascontiguousarray(sh_base[ct_of[:, None], ix]).reshape(-1)
+    from hydrabadger_amd import tdec_workload as tw
+    from hydrabadger_amd import threshold as th
+    t_gen = time.perf_counter()
+    ep = tw.make_epoch(ctx, dev, n_ct, N_NODES, 256, bad_rate, seed)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t_gen
+    N, t = ep.n_nodes, ep.t
+    n = n_ct * N
+    pt = torch.zeros(n_ct * ep.msg_len, dtype=torch.uint8, device=dev)
+    st = torch.zeros(n_ct, dtype=torch.int32, device=dev)
+    oc = torch.zeros((n_ct, N), dtype=torch.uint8, device=dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    sct = torch.arange(n_ct, dtype=torch.int32, device=dev).repeat_interleave(N)
+    spk = torch.arange(N, dtype=torch.int32, device=dev).repeat(n_ct)
+    A = _lib.HBG_DEVICE | _lib.HBG_ASYNC
 
-    def d(a):
-        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    dU, dW, dV, doff, dpk, dsh, dsct, dspk = (d(U), d(W), d(np.frombuffer(Vb, np.uint8)), d(off.view(np.int64)),
-                                              d(pk), d(share), d(sct.view(np.int32)), d(spk.view(np.int32)))
-    dix, dcsh = d(ix.view(np.int32)), d(csh)
-    ok = torch.empty(n_ct * n, dtype=torch.uint8, device=dev)
-    pt = torch.empty(max(int(off[-1]), 1), dtype=torch.uint8, device=dev)
-    st = torch.empty(n_ct, dtype=torch.int32, device=dev)
-    L = _lib.lib()
-    flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
+    def run():
+        th.threshold_decrypt_arrays(t, N, ep.U, ep.V, ep.V_off, ep.W, ep.pk48, ep.share48, None, pt, st, oc,
+                                    ctx=ctx, device=True, asynchronous=True)
 
     def verify():
-        _lib.check(L.hbg_tdec_verify_shares(ctx.h, n_ct, dU.data_ptr(), dV.data_ptr(), doff.data_ptr(),
-                                            dW.data_ptr(), n, dpk.data_ptr(), n_ct * n, dsh.data_ptr(),
-                                            dsct.data_ptr(), dspk.data_ptr(), ok.data_ptr(), flags), "verify")
-
-    def combine():
-        _lib.check(L.hbg_tdec_combine(ctx.h, t, n_ct, dcsh.data_ptr(), dix.data_ptr(), dV.data_ptr(),
-                                      doff.data_ptr(), pt.data_ptr(), st.data_ptr(), flags), "combine")
+        _lib.check(_lib.lib().hbg_tdec_verify_shares(ctx.h, n_ct, ep.U.data_ptr(), ep.V.data_ptr(),
+                                                     ep.V_off.data_ptr(), ep.W.data_ptr(), N, ep.pk48.data_ptr(), n,
+                                                     ep.share48.data_ptr(), sct.data_ptr(), spk.data_ptr(),
+                                                     ok.data_ptr(), A), "verify")
+    run()
     verify()
-    combine()
-    torch.cuda.synchronize()
-    bits_ok = bool(np.array_equal(ok.cpu().numpy(), expect))
-    ptb = pt.cpu().numpy().tobytes()
-    ref_pt = np.frombuffer(b"".join(bytes.fromhex(g["cts"][j % K]["plaintext"]) for j in range(n_ct)), np.uint8)
-    pts_ok = bool((st == 0).all().item()) and ptb == ref_pt.tobytes()
+    ctx.sync()
+    outcomes_ok = bool(np.array_equal(oc.cpu().numpy(), tw.expected_outcomes(ep.bad, t)))
+    bits_ok = bool(np.array_equal(ok.cpu().numpy().astype(bool), ~ep.bad.reshape(-1)))
+    pts_ok = bool((st == 0).all().item()) and bool(torch.equal(pt, ep.msgs))
+    ms = timed(run, reps)
     ms_v = timed(verify, reps)
-    ms_c = timed(combine, reps)
-    return {"metric": "TDec shares/s (verify_decryption_share) at N=64 t=21", "unit": "shares/s",
-            "value": n_ct * n / ((ms_v + ms_c) * 1e-3), "verify_shares_per_s": n_ct * n / (ms_v * 1e-3),
-            "combine_cts_per_s": n_ct / (ms_c * 1e-3), "verify_ms": ms_v, "combine_ms": ms_c,
-            "n_ct": n_ct, "shares": n_ct * n, "corrupted": int(bad.sum()),
-            "ok_bits_match": bits_ok, "plaintexts_match": pts_ok,
-            "inputs": "tests/golden/tdec_n64.json (4 ciphertexts x 64 shares) replicated, HBM-resident"}
+    kinds = {tw.BAD_KINDS[k]: int((ep.kind == k).sum()) for k in range(3)}
+    out = {"metric": "TDec shares/s (ThresholdDecrypt: ct verify + verify_decryption_share + select + decrypt) "
+                     "at N=64 t=21", "unit": "shares/s",
+           "value": n / (ms * 1e-3), "threshold_decrypt_ms": ms, "verify_ms": ms_v,
+           "verify_shares_per_s": n / (ms_v * 1e-3), "decrypt_cts_per_s": n_ct / (ms * 1e-3),
+           "n_ct": n_ct, "shares": n, "corrupted": int(ep.bad.sum()), "corrupted_by_kind": kinds,
+           "faults_reported": int((oc == _lib.HBG_SHARE_FAULTY).sum().item()),
+           "ok_bits_match": bits_ok, "outcomes_match": outcomes_ok, "plaintexts_match": pts_ok,
+           "inputs": f"distinct: {n_ct} ciphertexts of 256-B contributions encrypted on the device under a seeded "
+                     f"degree-{t} key set, all {N} decryption shares per ciphertext made on the device, "
+                     f"{bad_rate:.0%} replaced (three kinds); generated in {t_gen:.1f} s, HBM-resident"}
+    prof = fp_count_profile(N, t, bad_rate)
+    if prof:
+        per_share = prof["per_share_total"]
+        achieved = per_share * MADS_PER_FP_MUL * n / (ms * 1e-3)
+        per_share_v = prof.get("per_share_verify_total", per_share)
+        achieved_v = per_share_v * MADS_PER_FP_MUL * n / (ms_v * 1e-3)
+        out["roofline"] = {
+            "kernel": "hbg_tdec_threshold_decrypt (all its kernels; per-kernel counts in the profile)",
+            "bound": "valu", "unit": "T v_mad_u64_u32/s",
+            "achieved": achieved / 1e12, "peak": MAD_PEAK / 1e12, "frac": achieved / MAD_PEAK,
+            "fp_mul_per_share": per_share, "mads_per_fp_mul": MADS_PER_FP_MUL,
+            "verify_only": {"achieved": achieved_v / 1e12, "frac": achieved_v / MAD_PEAK,
+                            "fp_mul_per_share": per_share_v},
+            "traffic": None, "count_source": prof["path"] + " (" + prof.get("source", "") + ")",
+            "peak_source": "v_mad_u64_u32 4.44 cyc/wave-instr/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) "
+                           "x 1024 SIMDs x 64 lanes x 2.4 GHz",
+            "note": "each Fp mul also issues 288 v_addc (carry) + ~95 other VALU: frac <= ~0.5 by construction",
+            "occupancy": kernel_meta(["tdec_batch_leaves", "tdec_batch_check", "tdec_verify_shares",
+                                      "tdec_ct_prepare", "tdec_ct_verify", "tdec_combine_grp"]),
+        }
+    return out, ep
 
 
 def _dev_scalars(n: int, dev, seed: int):
@@ -310,8 +366,8 @@ def tdec_inputs_leg(ctx, dev, n_ct: int, n_nodes: int, reps: int):
     from hydrabadger_amd import _lib
     L = _lib.lib()
     flags = _lib.HBG_DEVICE | _lib.HBG_ASYNC
-    g = _tdec_fixture()
-    pk48 = torch.from_numpy(np.frombuffer(bytes.fromhex(g["cts"][0]["U"]), np.uint8).copy()).to(dev)  # any G1 point
+    from hydrabadger_amd import tdec_workload as tw
+    pk48 = torch.from_numpy(np.frombuffer(tw.G1_GENERATOR, np.uint8).copy()).to(dev)  # any G1 point
     msg_len = 256
     gen = torch.Generator(device="cpu").manual_seed(0x48424247)
     msgs = torch.randint(0, 256, (n_ct * msg_len,), dtype=torch.uint8, generator=gen).to(dev)
@@ -517,6 +573,7 @@ def network_leg(ctx, dev, n_nodes: int, reps: int):
 
 def main():
     a = parse()
+    legs = set(LEGS) if a.legs == "all" else set(a.legs.split(","))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -592,7 +649,7 @@ def main():
 
     # ---- decode path: reconstruct exactly 2f erasures + tree + glue ----
     decode = None
-    if not a.no_decode:
+    if not a.no_decode and "decode" in legs:
         from hydrabadger_amd import workload
         nd = min(B, 2048)
         present = torch.tensor([workload.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
@@ -615,30 +672,31 @@ def main():
                   "erased_per_instance": parity, "roundtrip_ok": ok}
 
     bwire = None
-    if a.wire_instances > 0:
+    if a.wire_instances > 0 and "bwire" in legs:
         bwire = broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps)
 
     epoch = None
-    if a.epoch_nodes > 0 and a.epoch_nodes % world == 0:
+    if a.epoch_nodes > 0 and a.epoch_nodes % world == 0 and "epoch" in legs:
         epoch = network_leg(ctx, dev, a.epoch_nodes, max(2, min(a.steps, 5)))
 
-    tdec = None
-    if a.tdec_cts > 0:
-        tdec = tdec_leg(ctx, dev, a.tdec_cts, 2)
+    tdec = tdec_ep = None
+    if a.tdec_cts > 0 and "tdec" in legs:
+        tdec, tdec_ep = tdec_leg(ctx, dev, a.tdec_cts, 2, seed=1 + rank)
         tdec["value"] = shard.sum_over_ranks(tdec["value"], dev)  # whole-job shares/s
 
     wire = tdec_in = None
-    if a.wire_msgs > 0:
+    if a.wire_msgs > 0 and "wire" in legs:
         wire = wire_leg(ctx, dev, a.wire_msgs, 256, 2)
-    if a.f1_cts > 0:
+    if a.f1_cts > 0 and "f1" in legs:
         tdec_in = tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2)
-    coin = coin_leg(ctx, dev, a.coins, N_NODES, 2) if a.coins > 0 else None
+    coin = coin_leg(ctx, dev, a.coins, N_NODES, 2) if a.coins > 0 and "coin" in legs else None
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a.cpu_sample)
+        if "rbc" in legs:
+            cpu = cpu_baseline(a.cpu_sample)
         if tdec is not None:
-            tdec["cpu_baseline"] = cpu_baseline_tdec()
+            tdec["cpu_baseline"] = cpu_baseline_tdec(tdec_ep)
 
     if rank == 0:
         line = {

@@ -30,12 +30,15 @@ HBG_E_SINGULAR_MATRIX = -17
 HBG_E_NOT_ENOUGH_SHARES = -20
 HBG_E_DUPLICATE_ENTRY = -21
 HBG_E_INVALID_POINT = -22
+HBG_E_INVALID_CIPHERTEXT = -23
 HBG_E_WIRE_EOF = -30
 HBG_E_WIRE_TAG = -31
 HBG_E_WIRE_FRAME = -32
 HBG_E_INVALID_SIGNATURE = -33
 HBG_E_UNKNOWN_PEER = -34
 HBG_WIRE_KIND_MESSAGE, HBG_WIRE_KIND_KEYGEN, HBG_WIRE_KIND_MAX = 7, 9, 10
+
+HBG_SHARE_NONE, HBG_SHARE_ACCEPTED, HBG_SHARE_FAULTY, HBG_SHARE_IGNORED = 0, 1, 2, 3
 
 HBG_MSG_VALUE, HBG_MSG_ECHO, HBG_MSG_READY, HBG_MSG_CAN_DECODE, HBG_MSG_ECHO_HASH = 0, 1, 2, 3, 4
 
@@ -78,6 +81,8 @@ SIGNATURES = {
     "hbg_tdec_verify_shares": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_ct_verify": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u32]),
     "hbg_tdec_combine": (_i, [_vp, _u32, _u32, _u8p, _vp, _u8p, _vp, _u8p, _vp, _u32]),
+    "hbg_tdec_threshold_decrypt": (_i, [_vp, _u32, _u32, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u8p, _vp, _u8p, _vp,
+                                        _u8p, _u32]),
     "hbg_tdec_encrypt": (_i, [_vp, _u8p, _u64, _u8p, _u8p, _vp, _u8p, _u8p, _u8p, _u32]),
     "hbg_tdec_decrypt_shares": (_i, [_vp, _u32, _u8p, _u32, _u8p, _u64, _vp, _vp, _u8p, _vp, _u32]),
     "hbg_bls_sign": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u32]),

@@ -26,7 +26,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 32;
+constexpr int kNumSlots = 40;
 
 struct Buf {
     void* p = nullptr;
@@ -230,6 +230,7 @@ const char* hbg_strerror(int code) {
         case HBG_E_NOT_ENOUGH_SHARES: return "NotEnoughShares";
         case HBG_E_DUPLICATE_ENTRY: return "DuplicateEntry";
         case HBG_E_INVALID_POINT: return "InvalidPoint";
+        case HBG_E_INVALID_CIPHERTEXT: return "InvalidCiphertext";
         case HBG_E_WIRE_EOF: return "UnexpectedEof";
         case HBG_E_WIRE_TAG: return "InvalidVariant";
         case HBG_E_WIRE_FRAME: return "FrameLength";
@@ -607,6 +608,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_CHECK(scratch(c, 21, tb_bytes, &temp));
     HBG_CHECK(scratch(c, 22, 64, &cnt));
     const uint32_t nb = bls::tdec_batch_bound(n, n_keys);
+    bls::tdec_debug_bounds(n, nb, n_keys, (uint64_t)n_pk + 1);
     void *sums, *lok, *items, *items2, *fails;
     HBG_CHECK(scratch(c, 23, (size_t)bls::kBatchSumBytes * nb, &sums));
     HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
@@ -810,6 +812,70 @@ int drain(hbg_ctx* c, uint32_t flags, std::initializer_list<std::pair<void*, std
 }
 constexpr uint64_t kVerifyChunk = 131072;  // messages per bls_verify launch (G2Prepared scratch: 39 KB each)
 }  // namespace
+
+int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_t n_ct, const uint8_t* U48,
+                               const uint8_t* V, const uint64_t* V_off, const uint8_t* W96, const uint8_t* pk48,
+                               const uint8_t* share48, const uint32_t* arrival, uint8_t* plaintext, int32_t* status,
+                               uint8_t* outcome, uint32_t flags) {
+    if (!c || (n_ct && (!U48 || !V_off || !W96 || !pk48 || !share48 || !status || !outcome || n_nodes == 0)))
+        return HBG_E_ARG;
+    if (n_ct == 0) return HBG_OK;
+    if (t >= n_nodes || n_ct == 0xFFFFFFFFu || n_nodes == 0xFFFFFFFFu) return HBG_E_ARG;
+    const uint64_t n = (uint64_t)n_ct * n_nodes, m = (uint64_t)t + 1;
+    if (n >= (1ull << 31)) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HBG_TRY(hipSetDevice(c->device));
+    CtTable tab;
+    const uint8_t* dV;
+    const uint64_t* dVoff;
+    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, tab, &dV, &dVoff));
+    const uint64_t vlen = (flags & HBG_DEVICE) ? 0 : V_off[n_ct];
+    if (!(flags & HBG_DEVICE) && vlen && !plaintext) return HBG_E_ARG;
+    const void *dpk, *dsh, *darr = nullptr;
+    void *dpt, *dst, *doc;
+    HBG_CHECK(stage_in(c, flags, 32, pk48, 48ull * n_nodes, &dpk));
+    HBG_CHECK(stage_in(c, flags, 33, share48, 48ull * n, &dsh));
+    if (arrival) HBG_CHECK(stage_in(c, flags, 34, arrival, 4ull * n, &darr));
+    HBG_CHECK(stage_out(c, flags, 35, plaintext, vlen, &dpt));
+    HBG_CHECK(stage_out(c, flags, 36, status, 4ull * n_ct, &dst));
+    HBG_CHECK(stage_out(c, flags, 37, outcome, n, &doc));
+    // set_ciphertext: Ciphertext::verify on the prepared table
+    void *ctok, *pairs, *okb, *sel;
+    HBG_CHECK(scratch(c, 30, n_ct, &ctok));
+    HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok, c->stream));
+    // verify_decryption_share of every (ct, sender) share, batched
+    HBG_CHECK(scratch(c, 15, 8ull * n, &pairs));
+    HBG_CHECK(scratch(c, 31, n, &okb));
+    uint32_t* sct = (uint32_t*)pairs;
+    uint32_t* spk = sct + n;
+    HBG_TRY(bls::launch_tdec_pair_index(n, n_nodes, sct, spk, c->stream));
+    void *paff, *pst;
+    HBG_CHECK(prepare_pks(c, n_nodes, (const uint8_t*)dpk, &paff, &pst));
+    if (c->tdec_batched && n >= 2) {
+        HBG_CHECK(verify_shares_batched(c, n_ct, tab, tab.U48, (uint32_t)n, n_nodes, (const uint8_t*)dsh, sct, spk,
+                                        (const uint32_t*)paff, (const int32_t*)pst, (uint8_t*)okb));
+    } else {
+        HBG_TRY(bls::launch_tdec_verify_shares(n, nullptr, (const uint8_t*)dsh, sct, spk, tab.ct_u, tab.ct_status,
+                                               tab.coefH, tab.coefW, (const uint32_t*)paff, (const int32_t*)pst,
+                                               (uint8_t*)okb, c->stream));
+    }
+    // handle_message / try_output: the first t+1 valid arrivals, faults, late shares
+    HBG_CHECK(scratch(c, 38, (4 + 48) * m * n_ct + 4ull * n_ct, &sel));
+    uint32_t* sidx = (uint32_t*)sel;
+    uint8_t* s48 = (uint8_t*)(sidx + m * n_ct);
+    int32_t* sst = (int32_t*)(s48 + 48 * m * n_ct);
+    HBG_TRY(bls::launch_tdec_select(n_ct, n_nodes, t, (const uint8_t*)ctok, (const uint8_t*)okb,
+                                    (const uint32_t*)darr, (const uint8_t*)dsh, sidx, s48, (uint8_t*)doc, sst,
+                                    c->stream));
+    // PublicKeySet::decrypt (interpolate + xor_with_hash) of the selections
+    void* scr;
+    HBG_CHECK(scratch(c, 39, 4ull * 32 * m * n_ct, &scr));
+    HBG_TRY(bls::launch_tdec_combine(n_ct, t, s48, sidx, dV, dVoff, (uint8_t*)dpt, (int32_t*)dst, (uint32_t*)scr,
+                                     c->stream));
+    HBG_TRY(bls::launch_tdec_status_merge(n_ct, sst, (int32_t*)dst, c->stream));
+    return drain(c, flags, {{plaintext, {dpt, vlen}}, {status, {dst, 4ull * n_ct}}, {outcome, {doc, n}}});
+}
+
 
 int hbg_bls_sign(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_t n, const uint32_t* msg_sk,
                  const uint8_t* msg, const uint64_t* msg_off, uint8_t* sig96, uint32_t flags) {

@@ -44,7 +44,24 @@ BD Fp fp_zero() {
 
 BD Fp fp_one() { return fp_const(kOne); }
 
+// Instrumented builds only (tools/fpcount.py compiles with -DHBG_FP_COUNT):
+// count the Fp multiplications / squarings every kernel executes, per active
+// lane (one wave-aggregated atomic per call), attributed per launch on the
+// host (tdec_kernels.hip HBG_COUNT_MARK).  The product library has no counter.
+#ifdef HBG_FP_COUNT
+__device__ unsigned long long g_fp_count[2];  // [0] fp_mul, [1] fp_sqr
+__device__ __forceinline__ void fp_count(int which) {
+    const uint64_t m = __builtin_amdgcn_read_exec();
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    if (lane == (uint32_t)__builtin_ctzll(m)) atomicAdd(&g_fp_count[which], (unsigned long long)__builtin_popcountll(m));
+}
+#define HBG_FP_COUNT_CALL(which) fp_count(which)
+#else
+#define HBG_FP_COUNT_CALL(which) ((void)0)
+#endif
+
 __device__ __noinline__ Fp fp_mul(Fp a, Fp b) {
+    HBG_FP_COUNT_CALL(0);
     uint32_t x[12], y[12], r[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
@@ -59,6 +76,7 @@ __device__ __noinline__ Fp fp_mul(Fp a, Fp b) {
 }
 
 __device__ __noinline__ Fp fp_sqr(Fp a) {
+    HBG_FP_COUNT_CALL(1);
     uint32_t x[12], r[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = a[i];

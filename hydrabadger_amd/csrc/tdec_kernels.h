@@ -42,6 +42,7 @@ hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_keys, const uint32_t* s
                                   uint32_t* perm, uint32_t* tmp_a, uint32_t* tmp_b, BatchDesc* desc, void* temp,
                                   size_t temp_bytes, uint32_t* nb_dev, hipStream_t st);
 uint32_t tdec_batch_bound(uint32_t n, uint32_t n_keys);  // upper bound of the batch count
+void tdec_debug_bounds(uint64_t n, uint64_t nb_max, uint64_t n_ct1, uint64_t n_pk1);  // -DHBG_DEBUG_CHECKS only
 hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_ct, const BatchDesc* desc,
                                     const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
                                     const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
@@ -88,6 +89,11 @@ hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const u
                                     hipStream_t st);
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
+hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8_t* ct_ok, const uint8_t* ok,
+                              const uint32_t* arrival, const uint8_t* share48, uint32_t* sel_idx, uint8_t* sel48,
+                              uint8_t* outcome, int32_t* sel_status, hipStream_t st);
+hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st);
+hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32_t* status, hipStream_t st);
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, hipStream_t st);

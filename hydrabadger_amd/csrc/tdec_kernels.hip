@@ -48,6 +48,20 @@ BD uint64_t dev_count(const uint32_t* n_dev, uint64_t cap) {
 BD uint64_t grid_lane() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 BD uint64_t grid_lanes() { return (uint64_t)gridDim.x * blockDim.x; }
 
+// Diagnostic builds only (-DHBG_DEBUG_CHECKS, tools/diag_tdec.py): range checks
+// on the batched verifier's indices that print and skip instead of faulting.
+#ifdef HBG_DEBUG_CHECKS
+__device__ uint64_t g_dbg[4];  // n shares, nb_max, n_ct + 1, n_pk + 1
+#define HBG_DBG_RANGE(v, bound, what)                                                                   \
+    (((uint64_t)(v) < (uint64_t)(bound))                                                                \
+         ? true                                                                                         \
+         : (printf("hbg range: %s = %llu >= %llu (%s:%d)\n", what, (unsigned long long)(v),              \
+                   (unsigned long long)(bound), __FILE__, __LINE__),                                    \
+            false))
+#else
+#define HBG_DBG_RANGE(v, bound, what) true
+#endif
+
 // ------------------------------------------------------------------ SHA3-256 over bytes
 BD void sha3_bytes(const uint8_t* p, uint32_t len, uint8_t out[32]) {
     u64p a[25];
@@ -455,7 +469,13 @@ TDEC_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restrict__ n
     const uint64_t n = dev_count(n_dev, cap);
     for (uint64_t i = grid_lane(); i < n; i += grid_lanes()) {
     const uint64_t k = sel ? sel[i] : i;  // sel: share indices (batched path's failing leaves)
+#ifdef HBG_DEBUG_CHECKS
+    if (!HBG_DBG_RANGE(k, g_dbg[0], "verify_shares k")) continue;
+#endif
     const uint32_t ct = share_ct[k], pk = share_pk[k];  // sanitised: invalid pairs point at the sentinels
+#ifdef HBG_DEBUG_CHECKS
+    if (!HBG_DBG_RANGE(ct, g_dbg[2], "verify_shares ct") || !HBG_DBG_RANGE(pk, g_dbg[3], "verify_shares pk")) continue;
+#endif
     bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
     G1A s;
     if (good) good = g1_decompress(share48 + 48ull * k, s, true);
@@ -605,7 +625,7 @@ BD G1 g1_mul_ab32(const Fp& px, const Fp& py, uint32_t a, uint32_t b) {
     return r;
 }
 
-TDEC_KERNEL void tdec_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t n_ct,
+TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_ct,
                                                         const BatchDesc* __restrict__ desc,
                                                         const uint32_t* __restrict__ perm,
                                                         const uint8_t* __restrict__ share48,
@@ -617,9 +637,16 @@ TDEC_KERNEL void tdec_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t
                                                         const uint32_t* __restrict__ pk_tbl,
                                                         uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
-    if (b >= *nb_dev) return;  // grid sized for the bound; the batch count is a device word
+    const uint32_t lane = threadIdx.x;
+    const uint64_t nb = dev_count(nb_dev, cap);  // the batch count is a device word
+    // block-stride over the batches on a resident grid
+    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const BatchDesc d = desc[b];
+#ifdef HBG_DEBUG_CHECKS
+    if (lane == 0 && (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "leaves d.end") || !HBG_DBG_RANGE(d.start, d.end, "leaves d.start") ||
+                      !HBG_DBG_RANGE(d.end - d.start, 65, "leaves size") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "leaves d.ct")))
+        printf("  batch %u of %u\n", (uint32_t)b, (uint32_t)nb);
+#endif
     const uint32_t q = d.start + lane;
     const bool in = q < d.end;
     const uint32_t k = in ? perm[q] : 0u;
@@ -696,6 +723,7 @@ TDEC_KERNEL void tdec_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t
         store_jac(out + kNodeBatch * kSumWords, A);
         store_jac(out + kNodeBatch * kSumWords + kJacWords, B);
     }
+    }
 }
 
 // Node geometry of a check item in its batch's 4-ary tree: leaf lanes [l0, l1).
@@ -754,7 +782,13 @@ TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_d
     const uint64_t n_items = dev_count(n_dev, cap);
     for (uint64_t i = grid_lane(); i < n_items; i += grid_lanes()) {
     const CheckItem it = items ? items[i] : CheckItem{(uint32_t)i, kNodeBatch};
+#ifdef HBG_DEBUG_CHECKS
+    if (!HBG_DBG_RANGE(it.b, g_dbg[1], "check it.b") || !HBG_DBG_RANGE(it.node, kNodes, "check node")) continue;
+#endif
     const BatchDesc d = desc[it.b];
+#ifdef HBG_DEBUG_CHECKS
+    if (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "check d.end") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "check d.ct")) continue;
+#endif
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
     const uint32_t l0 = node_first(it.node);
     if (!node_any_valid(lok, l0, l0 + node_size(it.node))) continue;  // nothing valid to vouch for: those shares stay 0
@@ -784,6 +818,94 @@ TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
                               coefH + (uint64_t)k * 72 * kMillerSteps, ux, nuy, !u_inf);
     }
     ok[k] = good ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- ThresholdDecrypt glue (a18)
+// hbbft ThresholdDecrypt [EXT, src/threshold_decrypt.rs] for one ciphertext of
+// the epoch, given every sender's share verdict (PublicKeyShare::
+// verify_decryption_share, computed for all shares by the batched verifier):
+//  * set_ciphertext: an invalid ciphertext (Ciphertext::verify false) is
+//    rejected — no shares are processed, no output;
+//  * handle_message(sender, share), in arrival order, until terminated: an
+//    invalid share is a fault (FaultKind::UnverifiedDecryptionShareSender), a
+//    valid one is held (a second message from a held or faulty sender
+//    changes nothing);
+//  * try_output fires as soon as more than f = t shares are held: it
+//    terminates and decrypts with the held shares (the BTreeMap of senders:
+//    node-id order) — so exactly the first t+1 valid arrivals;
+//  * shares arriving after termination are ignored (never checked).
+// One thread per ciphertext.  Outputs: the t+1 selected (index, share) pairs
+// sorted by node index for hbg_tdec_combine's kernel, a per-(ct, sender)
+// outcome byte and the selection status.
+__global__ __launch_bounds__(256) void tdec_select(uint32_t n_ct, uint32_t N, uint32_t t,
+                                                   const uint8_t* __restrict__ ct_ok, const uint8_t* __restrict__ ok,
+                                                   const uint32_t* __restrict__ arrival,
+                                                   const uint8_t* __restrict__ share48, uint32_t* __restrict__ sel_idx,
+                                                   uint8_t* __restrict__ sel48, uint8_t* __restrict__ outcome,
+                                                   int32_t* __restrict__ sel_status) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_ct) return;
+    const uint32_t m = t + 1;
+    uint8_t* oc = outcome + k * N;
+    uint32_t* idx = sel_idx + k * m;
+    for (uint32_t i = 0; i < N; ++i) oc[i] = HBG_SHARE_NONE;
+    uint32_t held = 0;
+    int32_t st = HBG_E_NOT_ENOUGH_SHARES;
+    if (!ct_ok[k]) {
+        st = HBG_E_INVALID_CIPHERTEXT;
+    } else {
+        bool term = false;
+        for (uint32_t j = 0; j < N; ++j) {
+            const uint32_t s = arrival ? arrival[k * N + j] : j;
+            if (s >= N) break;  // end of this ciphertext's arrivals
+            if (term) {
+                if (oc[s] == HBG_SHARE_NONE) oc[s] = HBG_SHARE_IGNORED;
+                continue;
+            }
+            if (oc[s] != HBG_SHARE_NONE) continue;
+            if (ok[k * N + s]) {
+                oc[s] = HBG_SHARE_ACCEPTED;
+                idx[held++] = s;
+                if (held == m) term = true;
+            } else {
+                oc[s] = HBG_SHARE_FAULTY;
+            }
+        }
+        if (term) st = 0;
+    }
+    uint32_t* dst = reinterpret_cast<uint32_t*>(sel48 + k * m * 48ull);
+    if (st != 0) {  // no output: a deterministic (invalid) selection
+        for (uint32_t q = 0; q < m; ++q) idx[q] = q;
+        for (uint32_t w = 0; w < 12 * m; ++w) dst[w] = 0;
+    } else {
+        for (uint32_t a = 1; a < m; ++a) {  // node-id order (the BTreeMap the crate iterates)
+            const uint32_t v = idx[a];
+            uint32_t b = a;
+            for (; b > 0 && idx[b - 1] > v; --b) idx[b] = idx[b - 1];
+            idx[b] = v;
+        }
+        for (uint32_t q = 0; q < m; ++q) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(share48 + (k * N + idx[q]) * 48ull);
+            for (int w = 0; w < 12; ++w) dst[12 * q + w] = src[w];
+        }
+    }
+    sel_status[k] = st;
+}
+
+// per-(ct, sender) verify work items of the epoch: share (k, i) -> ct k, key i
+__global__ __launch_bounds__(256) void tdec_pair_index(uint64_t n, uint32_t N, uint32_t* __restrict__ sct,
+                                                       uint32_t* __restrict__ spk) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    sct[q] = (uint32_t)(q / N);
+    spk[q] = (uint32_t)(q % N);
+}
+
+// status = selection status where it is not 0 (no output), else combine's
+__global__ __launch_bounds__(256) void tdec_status_merge(uint32_t n, const int32_t* __restrict__ sel_status,
+                                                         int32_t* __restrict__ status) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n && sel_status[k] != 0) status[k] = sel_status[k];
 }
 
 // ---------------------------------------------------------------- Fr (scalar field) for Lagrange
@@ -1452,15 +1574,17 @@ BD G2 g2_mul_ab32(const Fp2& px, const Fp2& py, uint32_t a, uint32_t b) {
     return r;
 }
 
-TDEC_KERNEL void sig_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t n_doc,
+TDEC_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_doc,
                                   const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                   const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_pk,
                                   const uint8_t* __restrict__ seeds, const uint32_t* __restrict__ pk_aff,
                                   const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ pk_tbl,
                                   uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
-    if (b >= *nb_dev) return;  // grid sized for the bound; the batch count is a device word
+    const uint32_t lane = threadIdx.x;
+    const uint64_t nb = dev_count(nb_dev, cap);  // the batch count is a device word
+    // block-stride over the batches on a resident grid
+    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const BatchDesc d = desc[b];
     const uint32_t q = d.start + lane;
     const bool in = q < d.end;
@@ -1535,6 +1659,7 @@ TDEC_KERNEL void sig_batch_leaves(const uint32_t* __restrict__ nb_dev, uint32_t 
                 store_g2jac(out + (kNode16 + (lane >> 4)) * kSigSumWords + kJacWords, A);
         }
         if (lane == 0) store_g2jac(out + kNodeBatch * kSigSumWords + kJacWords, A);
+    }
     }
 }
 
@@ -1689,14 +1814,48 @@ TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
 }
 
 // ------------------------------------------------------------------ launchers
+#ifdef HBG_FP_COUNT
+// Instrumented builds (tools/fpcount.py): every launcher first closes the
+// previous launch's count (stream sync + read/clear of g_fp_count) and
+// attributes it to that launch's kernel; hbg_fp_count_report() closes the
+// last one and returns {"kernel": [fp_mul, fp_sqr, launches], ...} as JSON.
+}  // namespace bls
+}  // namespace hbg
+#include <map>
+#include <string>
+namespace hbg {
+namespace bls {
+static std::map<std::string, uint64_t[3]> g_count_by_kernel;
+static std::string g_count_cur;
+static hipStream_t g_count_stream = nullptr;
+static void count_mark(const char* name, hipStream_t st) {
+    if (g_count_stream) (void)hipStreamSynchronize(g_count_stream);
+    unsigned long long v[2] = {0, 0};
+    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_fp_count), sizeof(v));
+    const unsigned long long z[2] = {0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fp_count), z, sizeof(z));
+    if (!g_count_cur.empty()) {
+        g_count_by_kernel[g_count_cur][0] += v[0];
+        g_count_by_kernel[g_count_cur][1] += v[1];
+    }
+    g_count_cur = name ? name : "";
+    g_count_stream = st;
+    if (name) g_count_by_kernel[g_count_cur][2] += 1;
+}
+#define HBG_COUNT_MARK(name, st) count_mark(name, st)
+#else
+#define HBG_COUNT_MARK(name, st) ((void)0)
+#endif
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
                                   uint32_t* coefW, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_ct_prepare", st);
     tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, W96, ct_u, ct_status, coefH, coefW);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st) {
+    HBG_COUNT_MARK("tdec_pk_prepare", st);
     tdec_pk_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, pk48, pk_aff, pk_status);
     return hipGetLastError();
 }
@@ -1712,6 +1871,7 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
                                      const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
                                      const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
                                      const uint32_t* sel) {
+    HBG_COUNT_MARK("tdec_verify_shares", st);
     if (cap == 0) return hipSuccess;
     tdec_verify_shares<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, share48, share_ct, share_pk, ct_u,
                                                                 ct_status, coefH, coefW, pk_aff, pk_status, ok, sel);
@@ -1721,6 +1881,7 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
 hipError_t launch_tdec_index_sanitize(uint64_t n, const uint32_t* a, uint32_t a_bound, const uint32_t* b,
                                       uint32_t b_bound, uint32_t* a_out, uint32_t* b_out, int32_t* err,
                                       hipStream_t st) {
+    HBG_COUNT_MARK("tdec_index_sanitize", st);
     if (n == 0) return hipSuccess;
     tdec_index_sanitize<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, a, a_bound, b, b_bound, a_out,
                                                                                b_out, err);
@@ -1743,6 +1904,7 @@ size_t tdec_batch_temp_bytes(uint32_t n) {
 hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_keys, const uint32_t* share_ct, uint32_t* keys,
                                   uint32_t* perm, uint32_t* tmp_a, uint32_t* tmp_b, BatchDesc* desc, void* temp,
                                   size_t temp_bytes, uint32_t* nb_dev, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_batch_plan", st);
     const dim3 g((n + 255) / 256), blk(256);
     int bits = 1;
     while (bits < 32 && (1ull << bits) < n_keys) ++bits;
@@ -1761,6 +1923,15 @@ hipError_t launch_tdec_batch_plan(uint32_t n, uint32_t n_keys, const uint32_t* s
     return hipMemcpyAsync(nb_dev, tmp_b + (n - 1), 4, hipMemcpyDeviceToDevice, st);
 }
 
+void tdec_debug_bounds(uint64_t n, uint64_t nb_max, uint64_t n_ct1, uint64_t n_pk1) {
+#ifdef HBG_DEBUG_CHECKS
+    const uint64_t v[4] = {n, nb_max, n_ct1, n_pk1};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), v, sizeof(v));
+#else
+    (void)n, (void)nb_max, (void)n_ct1, (void)n_pk1;
+#endif
+}
+
 uint32_t tdec_batch_bound(uint32_t n, uint32_t n_keys) {
     // sum over keys of ceil(count / 64) <= n / 64 + (number of distinct keys)
     const uint64_t distinct = n < n_keys ? n : n_keys;
@@ -1773,8 +1944,9 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
                                     uint8_t* leaf_ok, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
-    tdec_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
+    tdec_batch_leaves<<<dim3(nb_max < kResidentBlocks ? nb_max : kResidentBlocks), dim3(64), 0, st>>>(nb_max, nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
                                                          pk_aff, pk_status, pk_tbl, sums, leaf_ok);
     return hipGetLastError();
 }
@@ -1782,6 +1954,7 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
 size_t tdec_pk_table_bytes(uint32_t n_pk) { return 4ull * kPkTblWords * n_pk; }
 
 hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_pk_table", st);
     if (n_pk == 0) return hipSuccess;
     tdec_pk_table<<<dim3((n_pk * 2048u + 63) / 64), dim3(64), 0, st>>>(n_pk, pk_aff, tbl);
     return hipGetLastError();
@@ -1792,19 +1965,43 @@ hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const Ch
                                    const uint8_t* leaf_ok, const uint32_t* ct_u, const uint32_t* coefH,
                                    const uint32_t* coefW, uint8_t* ok, CheckItem* next, uint32_t* next_n,
                                    uint32_t* fail_list, uint32_t* fail_n, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_batch_check", st);
     if (cap == 0) return hipSuccess;
     tdec_batch_check<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, items, desc, perm, sums, leaf_ok, ct_u,
                                                               coefH, coefW, ok, next, next_n, fail_list, fail_n);
     return hipGetLastError();
 }
+hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8_t* ct_ok, const uint8_t* ok,
+                              const uint32_t* arrival, const uint8_t* share48, uint32_t* sel_idx, uint8_t* sel48,
+                              uint8_t* outcome, int32_t* sel_status, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_select", st);
+    if (n_ct == 0) return hipSuccess;
+    tdec_select<<<dim3((n_ct + 255) / 256), dim3(256), 0, st>>>(n_ct, N, t, ct_ok, ok, arrival, share48, sel_idx,
+                                                                 sel48, outcome, sel_status);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_pair_index", st);
+    if (n == 0) return hipSuccess;
+    tdec_pair_index<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, N, sct, spk);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32_t* status, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_status_merge", st);
+    if (n == 0) return hipSuccess;
+    tdec_status_merge<<<dim3((n + 255) / 256), dim3(256), 0, st>>>(n, sel_status, status);
+    return hipGetLastError();
+}
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_ct_verify", st);
     tdec_ct_verify<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, ct_u, ct_status, coefH, coefW, ok);
     return hipGetLastError();
 }
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     if (t + 1 <= 32)
         tdec_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status);
@@ -1815,6 +2012,7 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
 static dim3 grid64(uint64_t n) { return dim3((uint32_t)((n + 63) / 64)); }
 hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
                            const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st) {
+    HBG_COUNT_MARK("bls_sign", st);
     if (n == 0) return hipSuccess;
     bls_sign<<<grid64(n), dim3(64), 0, st>>>(n, n_sk, sk32, msg_sk, msg, off, sig96, err);
     return hipGetLastError();
@@ -1822,6 +2020,7 @@ hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const
 hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
                              const uint32_t* msg_pk, const uint8_t* msg, const uint64_t* off, const uint8_t* sig96,
                              uint32_t* lines, uint8_t* ok, int32_t* err, hipStream_t st) {
+    HBG_COUNT_MARK("bls_verify", st);
     if (n == 0) return hipSuccess;
     bls_verify<<<grid64(n), dim3(64), 0, st>>>(n, n_pk, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok, err);
     return hipGetLastError();
@@ -1829,6 +2028,7 @@ hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, 
 hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
                                      const uint32_t* frame_pk, const uint8_t* frames, const uint64_t* off,
                                      uint32_t* lines, int32_t* status, hipStream_t st) {
+    HBG_COUNT_MARK("wire_verify_frames", st);
     if (n == 0) return hipSuccess;
     wire_verify_frames<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, n_pk, frame_pk, frames, off, lines,
                                                        status);
@@ -1837,6 +2037,7 @@ hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const i
 hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
                                const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
                                int32_t* err, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_encrypt", st);
     if (n == 0) return hipSuccess;
     tdec_encrypt<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, r32, msg, off, U48, V, W96, err);
     return hipGetLastError();
@@ -1845,6 +2046,7 @@ hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, c
                                      const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
                                      const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
                                      hipStream_t st) {
+    HBG_COUNT_MARK("tdec_decrypt_share", st);
     if (n == 0) return hipSuccess;
     tdec_decrypt_share<<<grid64(n), dim3(64), 0, st>>>(n, n_ct, n_sk, u_aff, u_status, sk32, share_ct, share_sk,
                                                        share48, status, err);
@@ -1852,6 +2054,7 @@ hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, c
 }
 hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, const uint32_t* idx, uint8_t* sig96,
                                uint8_t* parity, int32_t* status, hipStream_t st) {
+    HBG_COUNT_MARK("coin_combine", st);
     if (n == 0) return hipSuccess;
     if (t + 1 > 32) return hipErrorInvalidValue;
     coin_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share96, idx, sig96, parity, status);
@@ -1859,6 +2062,7 @@ hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, c
 }
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,
                             uint32_t out_words, uint32_t* lines, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_test", st);
     tdec_test<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(op, n, in, out, in_words, out_words, lines);
     return hipGetLastError();
 }
@@ -1867,6 +2071,7 @@ hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* ou
 
 hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t* off, uint32_t* coefH,
                                   uint8_t* seeds, hipStream_t st) {
+    HBG_COUNT_MARK("sig_doc_prepare", st);
     if (n == 0) return hipSuccess;
     sig_doc_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, doc, off, coefH, seeds);
     return hipGetLastError();
@@ -1875,8 +2080,9 @@ hipError_t launch_sig_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint
                                    const uint32_t* perm, const uint8_t* share96, const uint32_t* share_pk,
                                    const uint8_t* seeds, const uint32_t* pk_aff, const int32_t* pk_status,
                                    const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, hipStream_t st) {
+    HBG_COUNT_MARK("sig_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
-    sig_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_dev, n_doc, desc, perm, share96, share_pk, seeds, pk_aff,
+    sig_batch_leaves<<<dim3(nb_max < kResidentBlocks ? nb_max : kResidentBlocks), dim3(64), 0, st>>>(nb_max, nb_dev, n_doc, desc, perm, share96, share_pk, seeds, pk_aff,
                                                         pk_status, pk_tbl, sums, leaf_ok);
     return hipGetLastError();
 }
@@ -1886,6 +2092,7 @@ hipError_t launch_sig_batch_check(uint32_t cap, const uint32_t* n_dev, uint32_t 
                                   const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
                                   CheckItem* next, uint32_t* next_n, uint32_t* fail_list, uint32_t* fail_n,
                                   hipStream_t st) {
+    HBG_COUNT_MARK("sig_batch_check", st);
     if (cap == 0) return hipSuccess;
     const uint64_t items_cap = items ? cap : (spec ? 5ull : 1ull) * cap;
     sig_batch_check<<<resident_grid(items_cap), dim3(64), 0, st>>>(cap, n_dev, spec, items, desc, perm, sums, leaf_ok,
@@ -1896,6 +2103,7 @@ hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const u
                                     const uint32_t* share_doc, const uint32_t* share_pk, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
                                     hipStream_t st) {
+    HBG_COUNT_MARK("sig_verify_shares", st);
     if (cap == 0) return hipSuccess;
     sig_verify_shares<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, sel, share96, share_doc, share_pk, pk_aff,
                                                                pk_status, coefH, lines, ok);
@@ -1904,3 +2112,22 @@ hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const u
 
 }  // namespace bls
 }  // namespace hbg
+
+#ifdef HBG_FP_COUNT
+extern "C" int hbg_fp_count_report(char* buf, uint64_t cap) {
+    using namespace hbg::bls;
+    count_mark(nullptr, nullptr);
+    std::string js = "{";
+    bool first = true;
+    for (auto& kv : g_count_by_kernel) {
+        js += (first ? "\"" : ", \"") + kv.first + "\": [" + std::to_string(kv.second[0]) + ", " +
+              std::to_string(kv.second[1]) + ", " + std::to_string(kv.second[2]) + "]";
+        first = false;
+    }
+    js += "}";
+    g_count_by_kernel.clear();
+    if (js.size() + 1 > cap) return -1;
+    memcpy(buf, js.c_str(), js.size() + 1);
+    return 0;
+}
+#endif

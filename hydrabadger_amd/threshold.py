@@ -7,6 +7,8 @@ as hbbft's ``ThresholdDecrypt`` uses it, reached from
   Ciphertext(U, V, W).verify()                         -> hbg_ct_verify          (a12)
   PublicKeyShare.verify_decryption_share(share, ct)    -> hbg_tdec_verify_shares (a14)
   PublicKeySet.decrypt(shares, ct)                     -> hbg_tdec_combine       (a15, a16)
+  ThresholdDecrypt (set_ciphertext, handle_message,
+    try_output) for a whole epoch                      -> hbg_tdec_threshold_decrypt (a18)
   PublicKey.encrypt_with_r(msg, r)                     -> hbg_tdec_encrypt       (§8 f1)
   SecretKey.decrypt_share_no_verify(ct)                -> hbg_tdec_decrypt_shares (§8 f1)
   SecretKey.sign(msg) / PublicKey.verify(sig, msg)     -> hbg_bls_sign / hbg_bls_verify (§8 f2,
@@ -128,6 +130,56 @@ class PublicKeySet:
         if st[0] != 0:
             raise HbgError(int(st[0]), "PublicKeySet::decrypt")
         return pts[0]
+
+
+# --------------------------------------------------------------------------- a18: ThresholdDecrypt glue
+SHARE_NONE, SHARE_ACCEPTED, SHARE_FAULTY, SHARE_IGNORED = (_lib.HBG_SHARE_NONE, _lib.HBG_SHARE_ACCEPTED,
+                                                           _lib.HBG_SHARE_FAULTY, _lib.HBG_SHARE_IGNORED)
+
+
+def threshold_decrypt_arrays(t: int, n_nodes: int, U, V, V_off, W, pk48, share48, arrival, plaintext, status,
+                             outcome, ctx=None, device: bool = False, asynchronous: bool = False) -> None:
+    """hbbft ThresholdDecrypt for a whole epoch (hbg_tdec_threshold_decrypt):
+    U [n_ct][48], W [n_ct][96], V bytes at V_off [n_ct+1], pk48 [N][48],
+    share48 [n_ct][N][48] (sender i's share of ct k at [k][i]), arrival
+    [n_ct][N] sender ids in arrival order or None (node order); outputs
+    plaintext (V layout), status [n_ct] i32, outcome [n_ct][N] u8.  Host
+    numpy arrays, or (device=True) CUDA tensors."""
+    n_ct = U.shape[0]
+    flags = (_lib.HBG_DEVICE if device else 0) | (_lib.HBG_ASYNC if asynchronous else 0)
+    check(lib().hbg_tdec_threshold_decrypt((ctx or default_context()).h, t, n_nodes, n_ct, ptr(U), ptr(V),
+                                           ptr(V_off), ptr(W), ptr(pk48), ptr(share48), ptr(arrival),
+                                           ptr(plaintext), ptr(status), ptr(outcome), flags), "ThresholdDecrypt")
+
+
+def threshold_decrypt_batch(t: int, cts: list, pk_shares: list, shares: list, arrivals=None, ctx=None):
+    """One node's ThresholdDecrypt instances for an epoch's ciphertexts:
+    shares[k][i] = sender i's 48-B share of cts[k] (None: never sent);
+    arrivals[k] = sender ids in arrival order (None: node order).  Returns
+    (plaintexts (None where status != 0), status array, outcome [n_ct][N])."""
+    n_ct, n = len(cts), len(pk_shares)
+    if n_ct == 0:
+        return [], np.zeros(0, np.int32), np.zeros((0, n), np.uint8)
+    U, V, off, W = _ct_table(cts)
+    pk = np.frombuffer(b"".join(bytes(p) for p in pk_shares), np.uint8).copy().reshape(n, 48)
+    sh = np.zeros((n_ct, n, 48), np.uint8)
+    arr = None
+    if arrivals is not None or any(x is None for row in shares for x in row):
+        arr = np.full((n_ct, n), 0xFFFFFFFF, np.uint32)
+    for k in range(n_ct):
+        order = list(range(n)) if arrivals is None or arrivals[k] is None else list(arrivals[k])
+        sent = [i for i in order if i < n and shares[k][i] is not None]
+        for i in range(n):
+            if shares[k][i] is not None:
+                sh[k, i] = np.frombuffer(bytes(shares[k][i]), np.uint8)
+        if arr is not None:
+            arr[k, :len(sent)] = sent
+    pt = np.zeros(max(int(off[-1]), 1), np.uint8)
+    st = np.zeros(n_ct, np.int32)
+    oc = np.zeros((n_ct, n), np.uint8)
+    threshold_decrypt_arrays(t, n, U, V, off, W, pk, sh, arr, pt, st, oc, ctx)
+    pts = [pt[int(off[k]):int(off[k + 1])].tobytes() if st[k] == 0 else None for k in range(n_ct)]
+    return pts, st, oc
 
 
 def test_bls(op: int, inputs: np.ndarray, out_words: int, ctx=None) -> np.ndarray:

@@ -218,3 +218,48 @@ def public_key_share(commitment: list, i: int):
     for c in reversed(commitment):
         acc = B.g1_add(B.g1_mul(acc, x) if acc is not None else None, c)
     return acc
+
+
+# ----------------------------------------------------------------------------- a18: ThresholdDecrypt glue
+SHARE_NONE, SHARE_ACCEPTED, SHARE_FAULTY, SHARE_IGNORED = 0, 1, 2, 3
+E_NOT_ENOUGH_SHARES, E_INVALID_CIPHERTEXT = -20, -23
+
+
+def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arrival=None):
+    """One node's hbbft ThresholdDecrypt instance [EXT, hbbft
+    src/threshold_decrypt.rs], restated:
+    set_ciphertext rejects an invalid ciphertext; handle_message(sender,
+    share) in arrival order faults an invalid share
+    (UnverifiedDecryptionShareSender) and holds a valid one until try_output
+    fires with more than t held (so: the first t+1 valid arrivals), which
+    terminates the instance and decrypts with the held shares in node-id
+    order (BTreeMap); later shares are ignored.
+    shares[i]: sender i's share (G1 point or None); arrival: sender ids in
+    arrival order (None: 0..N-1).  Returns (status, plaintext or None,
+    outcome per sender)."""
+    n = len(pk_shares)
+    order = list(range(n)) if arrival is None else list(arrival)
+    outcome = [SHARE_NONE] * n
+    if not ct.verify():
+        return E_INVALID_CIPHERTEXT, None, outcome
+    h = hash_g1_g2(ct.U, ct.V)
+    held = {}
+    for s in order:
+        if s >= n:
+            break
+        if len(held) == t + 1:
+            if outcome[s] == SHARE_NONE:
+                outcome[s] = SHARE_IGNORED
+            continue
+        if outcome[s] != SHARE_NONE:
+            continue
+        sh = shares[s]
+        valid = sh is not None and verify_decryption_share(pk_shares[s], sh, ct, h)
+        if valid:
+            outcome[s] = SHARE_ACCEPTED
+            held[s] = sh
+        else:
+            outcome[s] = SHARE_FAULTY
+    if len(held) < t + 1:
+        return E_NOT_ENOUGH_SHARES, None, outcome
+    return 0, decrypt(t, sorted(held.items()), ct), outcome

@@ -1,0 +1,200 @@
+"""hbbft ThresholdDecrypt glue, batched over an epoch.
+
+The oracle (oracle/tcrypto.py threshold_decrypt) restates hbbft's
+set_ciphertext / handle_message / try_output; CPU tests pin its semantics on
+hand-built cases (first t+1 valid arrivals, faults before termination, late
+shares ignored, NotEnoughShares, rejected ciphertext).  GPU tests run
+hbg_tdec_threshold_decrypt through the C ABI and must match the oracle's
+status, per-sender outcome and plaintext exactly, including seeded random
+arrival orders with the three corruption kinds of the bench.
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as B
+from oracle import tcrypto as T
+from tests import tdec_fixtures as fx
+
+ACC, FLT, IGN, NONE = T.SHARE_ACCEPTED, T.SHARE_FAULTY, T.SHARE_IGNORED, T.SHARE_NONE
+
+
+def _case(seed=5):
+    return fx.scenario(7, 3, 40, seed=seed)
+
+
+# ------------------------------------------------------------------ oracle semantics (CPU)
+def test_oracle_first_t_plus_one_valid_arrivals():
+    sc = _case()
+    t, ct, pks = sc["t"], sc["cts"][0], sc["pk_shares"]
+    shares = list(sc["shares"][0])
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares)
+    assert st == 0 and pt == sc["msgs"][0]
+    assert oc == [ACC] * (t + 1) + [IGN] * (7 - t - 1)
+    # a bad share before termination is a fault; the next valid one is taken instead
+    shares[1] = B.g1_add(shares[1], B.G1)
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares)
+    assert st == 0 and pt == sc["msgs"][0]
+    assert oc == [ACC, FLT, ACC, ACC, IGN, IGN, IGN]
+    # arrival order decides which shares are held; a repeated sender changes nothing
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[6, 6, 1, 5, 0, 3, 2])
+    assert st == 0 and pt == sc["msgs"][0]
+    assert oc == [ACC, FLT, IGN, IGN, NONE, ACC, ACC]
+
+
+def test_oracle_not_enough_and_invalid_ciphertext():
+    sc = _case()
+    t, ct, pks = sc["t"], sc["cts"][1], sc["pk_shares"]
+    shares = list(sc["shares"][1])
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[0, 4])
+    assert st == T.E_NOT_ENOUGH_SHARES and pt is None and oc == [ACC, NONE, NONE, NONE, ACC, NONE, NONE]
+    bad_ct = T.Ciphertext(ct.U, ct.V, B.g2_mul(ct.W, 2))
+    st, pt, oc = T.threshold_decrypt(t, bad_ct, pks, shares)
+    assert st == T.E_INVALID_CIPHERTEXT and oc == [NONE] * 7
+
+
+# ------------------------------------------------------------------ GPU vs oracle
+def _th():
+    from hydrabadger_amd import threshold as th
+    return th
+
+
+def _corrupt(kind, k, i, sc, rng):
+    """The bench's three corruption kinds for sender i's share of ct k."""
+    n_ct, n = len(sc["cts"]), len(sc["pk_shares"])
+    if kind == 0:   # another node's share (claimed under the wrong key)
+        return sc["shares"][k][(i + 1) % n]
+    if kind == 1:   # the same node's share of another ciphertext
+        return sc["shares"][(k + 1) % n_ct][i]
+    return B.g1_mul(B.G1, rng.randrange(1, B.R))   # a random valid point
+
+
+@pytest.mark.gpu
+def test_gpu_glue_matches_oracle_hand_cases():
+    th = _th()
+    sc = _case()
+    t, pks = sc["t"], [B.g1_compress(p) for p in sc["pk_shares"]]
+    ct0, ct1, ct2 = sc["cts"]
+    bad_ct = T.Ciphertext(ct2.U, ct2.V, B.g2_mul(ct2.W, 2))
+    cts = [ct0, ct0, ct1, bad_ct]
+    sh = [list(sc["shares"][0]), list(sc["shares"][0]), list(sc["shares"][1]), list(sc["shares"][2])]
+    sh[1][1] = B.g1_add(sh[1][1], B.G1)
+    arrivals = [None, [6, 6, 1, 5, 0, 3, 2], [0, 4], None]
+    pts, st, oc = th.threshold_decrypt_batch(
+        t, [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in cts], pks,
+        [[B.g1_compress(x) for x in row] for row in sh], arrivals)
+    for k in range(4):
+        rst, rpt, roc = T.threshold_decrypt(t, cts[k], sc["pk_shares"], sh[k], arrivals[k])
+        assert st[k] == rst and list(oc[k]) == roc and pts[k] == rpt, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_gpu_glue_random_epochs_match_oracle(seed):
+    """16 nodes (t = 5), 12 ciphertexts: seeded arrival orders (some lists cut
+    short), ~15 % of the shares corrupted with the three kinds, one
+    ciphertext with fewer than t+1 valid arrivals."""
+    th = _th()
+    rng = random.Random(seed)
+    sc = fx.scenario(16, 12, 48, seed=20 + seed)
+    t, n, n_ct = sc["t"], 16, 12
+    shares, arrivals = [], []
+    for k in range(n_ct):
+        row = []
+        for i in range(n):
+            row.append(_corrupt(rng.randrange(3), k, i, sc, rng) if rng.random() < 0.15 else sc["shares"][k][i])
+        order = list(range(n))
+        rng.shuffle(order)
+        if k % 4 == 3:
+            order = order[: rng.randrange(t + 1, n)]
+        shares.append(row)
+        arrivals.append(order)
+    arrivals[5] = [i for i in arrivals[5]][: t]          # never enough
+    cts = [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in sc["cts"]]
+    # senders missing from a cut arrival list never sent
+    sent = [[x if i in set(arrivals[k]) else None for i, x in enumerate(shares[k])] for k in range(n_ct)]
+    pts, st, oc = th.threshold_decrypt_batch(t, cts, [B.g1_compress(p) for p in sc["pk_shares"]],
+                                             [[None if x is None else B.g1_compress(x) for x in row] for row in sent],
+                                             arrivals)
+    for k in range(n_ct):
+        rst, rpt, roc = T.threshold_decrypt(t, sc["cts"][k], sc["pk_shares"], shares[k], arrivals[k])
+        assert (int(st[k]), list(oc[k]), pts[k]) == (rst, roc, rpt), k
+    assert int(st[5]) == T.E_NOT_ENOUGH_SHARES
+
+
+@pytest.mark.gpu
+def test_gpu_glue_device_mode_async():
+    """Device tensors, HBG_ASYNC: same answers as the host-mode call."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import _lib
+    th = _th()
+    sc = fx.scenario(16, 4, 64, seed=9)
+    t, n, n_ct = sc["t"], 16, 4
+    cts = [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in sc["cts"]]
+    U, V, off, W = th._ct_table(cts)
+    pk = np.frombuffer(b"".join(B.g1_compress(p) for p in sc["pk_shares"]), np.uint8).copy()
+    sh = np.frombuffer(b"".join(B.g1_compress(sc["shares"][k][i]) for k in range(n_ct) for i in range(n)),
+                       np.uint8).copy().reshape(n_ct, n, 48)
+    sh[2, 3] = sh[2, 4]
+    dev = torch.device("cuda:0")
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pt = torch.zeros(int(off[-1]), dtype=torch.uint8, device=dev)
+    st = torch.zeros(n_ct, dtype=torch.int32, device=dev)
+    oc = torch.zeros((n_ct, n), dtype=torch.uint8, device=dev)
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    th.threshold_decrypt_arrays(t, n, d(U), d(V), d(off.view(np.int64)), d(W), d(pk), d(sh), None, pt, st, oc,
+                                ctx=ctx, device=True, asynchronous=True)
+    ctx.sync()
+    pts_h, st_h, oc_h = th.threshold_decrypt_batch(t, cts, [B.g1_compress(p) for p in sc["pk_shares"]],
+                                                   [[sh[k, i].tobytes() for i in range(n)] for k in range(n_ct)])
+    assert st.cpu().tolist() == st_h.tolist() == [0] * n_ct
+    assert np.array_equal(oc.cpu().numpy(), oc_h)
+    assert oc_h[2, 3] == FLT
+    assert pt.cpu().numpy().tobytes() == b"".join(sc["msgs"])
+
+
+@pytest.mark.gpu
+def test_device_generated_epoch_and_driver():
+    """hydrabadger_amd/tdec_workload.py (the bench's TDec inputs): key shares,
+    distinct ciphertexts and shares made on the device match the oracle for
+    a sample, and the driver's outcomes / plaintexts equal construction."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import _lib, tdec_workload as tw
+    th = _th()
+    dev = torch.device("cuda:0")
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ep = tw.make_epoch(ctx, dev, n_ct=96, n_nodes=16, msg_len=200, bad_rate=0.08, seed=3)
+    coeffs, sks = tw.keyset(16, ep.t, 3)
+    assert ep.pk48[5].cpu().numpy().tobytes() == B.g1_compress(B.g1_mul(B.G1, sks[5]))
+    assert ep.master_pk48.cpu().numpy().tobytes() == B.g1_compress(B.g1_mul(B.G1, coeffs[0]))
+    assert len(set(map(bytes, ep.U.cpu().numpy()))) == 96                     # distinct ciphertexts
+    k = 17
+    ct = T.Ciphertext(B.g1_decompress(ep.U[k].cpu().numpy().tobytes()), ep.V[200 * k:200 * k + 200].cpu().numpy().tobytes(),
+                      B.g2_decompress(ep.W[k].cpu().numpy().tobytes()))
+    assert ct.verify()
+    assert T.decrypt(ep.t, [(i, T.decrypt_share(sks[i], ct)) for i in range(ep.t + 1)], ct) == \
+        ep.msgs[200 * k:200 * k + 200].cpu().numpy().tobytes()
+    for (kk, ii) in list(zip(*np.nonzero(ep.bad)))[:6]:                       # replaced shares do not verify
+        ck = T.Ciphertext(B.g1_decompress(ep.U[kk].cpu().numpy().tobytes()),
+                          ep.V[200 * kk:200 * kk + 200].cpu().numpy().tobytes(),
+                          B.g2_decompress(ep.W[kk].cpu().numpy().tobytes()))
+        s = B.g1_decompress(ep.share48[kk, ii].cpu().numpy().tobytes())
+        assert not T.verify_decryption_share(B.g1_mul(B.G1, sks[ii]), s, ck)
+    assert set(np.unique(ep.kind[ep.bad])) == {0, 1, 2}
+    pt = torch.zeros(96 * 200, dtype=torch.uint8, device=dev)
+    st = torch.zeros(96, dtype=torch.int32, device=dev)
+    oc = torch.zeros((96, 16), dtype=torch.uint8, device=dev)
+    th.threshold_decrypt_arrays(ep.t, 16, ep.U, ep.V, ep.V_off, ep.W, ep.pk48, ep.share48, None, pt, st, oc,
+                                ctx=ctx, device=True)
+    assert st.cpu().tolist() == [0] * 96
+    assert np.array_equal(oc.cpu().numpy(), tw.expected_outcomes(ep.bad, ep.t))
+    assert torch.equal(pt, ep.msgs)
