@@ -64,6 +64,22 @@ namespace {
         if (r_ != HBG_OK) return r_; \
     } while (0)
 
+// Diagnostic builds only (-DHBG_DEBUG_CHECKS): synchronise after a launch and
+// name it on stderr, so a faulting kernel is the last step printed.
+#ifdef HBG_DEBUG_CHECKS
+#define HBG_DBG_STEP(c, name)                                                                  \
+    do {                                                                                       \
+        const hipError_t e_ = hipStreamSynchronize((c)->stream);                               \
+        fprintf(stderr, "[hbg step] %s: %s\n", name, hipGetErrorString(e_));                   \
+        fflush(stderr);                                                                        \
+        if (e_ != hipSuccess) return HBG_E_DEVICE;                                             \
+    } while (0)
+#else
+#define HBG_DBG_STEP(c, name) \
+    do {                      \
+    } while (0)
+#endif
+
 uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 // Grow-only device scratch slot (synchronises the stream before freeing).
@@ -596,6 +612,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
         HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
         tbl = (uint32_t*)p;
         HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream));
+        HBG_DBG_STEP(c, "pk_table");
     }
     const uint32_t n_keys = n_ct + 1;  // + the sentinel ciphertext
     void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
@@ -625,21 +642,64 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_TRY(hipMemsetAsync(counts, 0, 12, c->stream));
     HBG_TRY(bls::launch_tdec_batch_plan(n, n_keys, dsc, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta,
                                         (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, counts + 3, c->stream));
+    HBG_DBG_STEP(c, "batch_plan");
+#ifdef HBG_DEBUG_CHECKS
+    {  // host validation of the plan (sorted keys, permutation, batch cuts)
+        std::vector<uint32_t> hk(n), hp(n), hs(n), hnb(1);
+        struct HD {
+            uint32_t start, end, ct, pad;
+        };  // bls::BatchDesc's layout (kBatchDescBytes)
+        std::vector<HD> hd(nb);
+        HBG_TRY(hipMemcpy(hk.data(), keys, 4ull * n, hipMemcpyDeviceToHost));
+        HBG_TRY(hipMemcpy(hp.data(), perm, 4ull * n, hipMemcpyDeviceToHost));
+        HBG_TRY(hipMemcpy(hs.data(), dsc, 4ull * n, hipMemcpyDeviceToHost));
+        HBG_TRY(hipMemcpy(hnb.data(), counts + 3, 4, hipMemcpyDeviceToHost));
+        const uint32_t m = hnb[0] <= nb ? hnb[0] : nb;
+        HBG_TRY(hipMemcpy(hd.data(), desc, sizeof(HD) * m, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> seen(n, 0);
+        const char* bad = nullptr;
+        uint64_t at = 0;
+        for (uint64_t i = 0; i < n && !bad; ++i) {
+            if (hp[i] >= n || seen[hp[i]]) bad = "perm", at = i;
+            else if (seen[hp[i]] = 1, hs[hp[i]] != hk[i]) bad = "key/perm", at = i;
+            else if (i && hk[i] < hk[i - 1]) bad = "unsorted", at = i;
+            else if (hk[i] >= n_keys) bad = "key range", at = i;
+        }
+        uint32_t expect = 0;
+        for (uint32_t b = 0; b < m && !bad; ++b) {
+            const auto& d = hd[b];
+            if (d.start != expect || d.end <= d.start || d.end - d.start > bls::kBatchShares || d.end > n ||
+                d.ct != hk[d.start] || hk[d.end - 1] != d.ct)
+                bad = "desc", at = b;
+            expect = d.end;
+        }
+        if (!bad && expect != n) bad = "coverage", at = expect;
+        fprintf(stderr, "[hbg plan] n=%u keys=%u nb=%u bound=%u: %s at %llu\n", n, n_keys, hnb[0], nb,
+                bad ? bad : "ok", (unsigned long long)at);
+        fflush(stderr);
+        if (bad || hnb[0] > nb) return HBG_E_DEVICE;
+    }
+#endif
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.ct_status, paff, pst, tbl,
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream));
+    HBG_DBG_STEP(c, "batch_leaves");
     // round 0: every batch sum; failing batches push their 16-share groups
     HBG_TRY(bls::launch_tdec_batch_check(nb, counts + 3, nullptr, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it1,
                                          counts, (uint32_t*)fails, counts + 1, c->stream));
+    HBG_DBG_STEP(c, "check round 0");
     // round 1: 16-share groups; failing ones push their quads
     HBG_TRY(bls::launch_tdec_batch_check(4 * nb, counts, it1, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it2,
                                          counts + 2, (uint32_t*)fails, counts + 1, c->stream));
+    HBG_DBG_STEP(c, "check round 1");
     // round 2: quads; failing ones append their shares
     HBG_TRY(bls::launch_tdec_batch_check(16 * nb, counts + 2, it2, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok,
                                          nullptr, nullptr, (uint32_t*)fails, counts + 1, c->stream));
+    HBG_DBG_STEP(c, "check round 2");
     // round 3: the shares of failing quads, one by one (the reference's equation)
     HBG_TRY(bls::launch_tdec_verify_shares(n, counts + 1, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff,
                                            pst, dok, c->stream, (const uint32_t*)fails));
+    HBG_DBG_STEP(c, "per-share round");
     return HBG_OK;
 }
 
@@ -668,6 +728,7 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     const uint8_t* dV;
     const uint64_t* dVoff;
     HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, t, &dV, &dVoff));
+    HBG_DBG_STEP(c, "ct_prepare");
     const uint8_t *dpk = pk48, *dsh = share48;
     const uint32_t *dsc = share_ct, *dsp = share_pk;
     uint8_t* dok = ok;
@@ -694,11 +755,13 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
         uint32_t* sc2 = (uint32_t*)san;
         uint32_t* sp2 = sc2 + n;
         HBG_TRY(bls::launch_tdec_index_sanitize(n, share_ct, n_ct, share_pk, n_pk, sc2, sp2, c->d_err, c->stream));
+        HBG_DBG_STEP(c, "index_sanitize");
         dsc = sc2;
         dsp = sp2;
     }
     void *paff, *pst;
     HBG_CHECK(prepare_pks(c, n_pk, dpk, &paff, &pst));
+    HBG_DBG_STEP(c, "pk_prepare");
     if (c->tdec_batched && n >= 2 && n < (1ull << 31)) {
         HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, n_pk, dsh, dsc, dsp, (const uint32_t*)paff,
                                         (const int32_t*)pst, dok));

@@ -16,9 +16,9 @@ struct BatchDesc;
 struct CheckItem;
 constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 21 * 2 * 36 * 4;
 constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G2 Jacobian sums of 21 tree nodes
-// Grid-stride check rounds run on at most this many 64-lane blocks (2 waves
-// per SIMD x 1,024 SIMDs: the TDec kernels' resident limit); per-lane scratch
-// (G2Prepared lines) is sized for kResidentBlocks * 64 lanes.
+// The sig_* check rounds run in launches of at most kResidentBlocks 64-lane
+// blocks (2 waves per SIMD x 1,024 SIMDs: the TDec kernels' resident limit);
+// their per-lane scratch (G2Prepared lines) is sized for kResidentBlocks * 64.
 constexpr uint32_t kResidentBlocks = 2048;
 
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,

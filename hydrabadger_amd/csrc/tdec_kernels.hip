@@ -46,7 +46,6 @@ BD uint64_t dev_count(const uint32_t* n_dev, uint64_t cap) {
     return v < cap ? v : cap;
 }
 BD uint64_t grid_lane() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
-BD uint64_t grid_lanes() { return (uint64_t)gridDim.x * blockDim.x; }
 
 // Diagnostic builds only (-DHBG_DEBUG_CHECKS, tools/diag_tdec.py): range checks
 // on the batched verifier's indices that print and skip instead of faulting.
@@ -466,15 +465,15 @@ TDEC_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restrict__ n
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const int32_t* __restrict__ pk_status,
                                                          uint8_t* __restrict__ ok, const uint32_t* __restrict__ sel) {
-    const uint64_t n = dev_count(n_dev, cap);
-    for (uint64_t i = grid_lane(); i < n; i += grid_lanes()) {
+    const uint64_t i = grid_lane();
+    if (i >= dev_count(n_dev, cap)) return;
     const uint64_t k = sel ? sel[i] : i;  // sel: share indices (batched path's failing leaves)
 #ifdef HBG_DEBUG_CHECKS
-    if (!HBG_DBG_RANGE(k, g_dbg[0], "verify_shares k")) continue;
+    if (!HBG_DBG_RANGE(k, g_dbg[0], "verify_shares k")) return;
 #endif
     const uint32_t ct = share_ct[k], pk = share_pk[k];  // sanitised: invalid pairs point at the sentinels
 #ifdef HBG_DEBUG_CHECKS
-    if (!HBG_DBG_RANGE(ct, g_dbg[2], "verify_shares ct") || !HBG_DBG_RANGE(pk, g_dbg[3], "verify_shares pk")) continue;
+    if (!HBG_DBG_RANGE(ct, g_dbg[2], "verify_shares ct") || !HBG_DBG_RANGE(pk, g_dbg[3], "verify_shares pk")) return;
 #endif
     bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
     G1A s;
@@ -488,7 +487,6 @@ TDEC_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restrict__ n
                               coefW + (uint64_t)ct * 72 * kMillerSteps, pkx, pky, !pk_inf && !w_inf);
     }
     ok[k] = good ? 1 : 0;
-    }
 }
 
 // Device-mode index check of (ciphertext/document, key) pairs: an out-of-range
@@ -637,15 +635,13 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
                                                         const uint32_t* __restrict__ pk_tbl,
                                                         uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t nb = dev_count(nb_dev, cap);  // the batch count is a device word
-    // block-stride over the batches on a resident grid
-    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= dev_count(nb_dev, cap)) return;  // grid sized for the bound; the batch count is a device word
     const BatchDesc d = desc[b];
 #ifdef HBG_DEBUG_CHECKS
     if (lane == 0 && (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "leaves d.end") || !HBG_DBG_RANGE(d.start, d.end, "leaves d.start") ||
                       !HBG_DBG_RANGE(d.end - d.start, 65, "leaves size") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "leaves d.ct")))
-        printf("  batch %u of %u\n", (uint32_t)b, (uint32_t)nb);
+        printf("  batch %u of %u\n", b, *nb_dev);
 #endif
     const uint32_t q = d.start + lane;
     const bool in = q < d.end;
@@ -723,7 +719,6 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
         store_jac(out + kNodeBatch * kSumWords, A);
         store_jac(out + kNodeBatch * kSumWords + kJacWords, B);
     }
-    }
 }
 
 // Node geometry of a check item in its batch's 4-ary tree: leaf lanes [l0, l1).
@@ -767,7 +762,8 @@ BD void batch_tree_step(bool pass, const CheckItem& it, const BatchDesc& d, cons
 
 // One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.  Items:
 // the list `items` (count *n_dev) or, with items == null, every batch
-// (count *n_dev = the batch count); grid-stride over a resident grid.
+// (count *n_dev = the batch count); the grid covers `cap` items, lanes past
+// the device count return at once.
 TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, const CheckItem* __restrict__ items,
                                                        const BatchDesc* __restrict__ desc,
                                                        const uint32_t* __restrict__ perm,
@@ -779,19 +775,19 @@ TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_d
                                                        CheckItem* __restrict__ next, uint32_t* __restrict__ next_n,
                                                        uint32_t* __restrict__ fail_list,
                                                        uint32_t* __restrict__ fail_n) {
-    const uint64_t n_items = dev_count(n_dev, cap);
-    for (uint64_t i = grid_lane(); i < n_items; i += grid_lanes()) {
+    const uint64_t i = grid_lane();
+    if (i >= dev_count(n_dev, cap)) return;
     const CheckItem it = items ? items[i] : CheckItem{(uint32_t)i, kNodeBatch};
 #ifdef HBG_DEBUG_CHECKS
-    if (!HBG_DBG_RANGE(it.b, g_dbg[1], "check it.b") || !HBG_DBG_RANGE(it.node, kNodes, "check node")) continue;
+    if (!HBG_DBG_RANGE(it.b, g_dbg[1], "check it.b") || !HBG_DBG_RANGE(it.node, kNodes, "check node")) return;
 #endif
     const BatchDesc d = desc[it.b];
 #ifdef HBG_DEBUG_CHECKS
-    if (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "check d.end") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "check d.ct")) continue;
+    if (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "check d.end") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "check d.ct")) return;
 #endif
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
     const uint32_t l0 = node_first(it.node);
-    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) continue;  // nothing valid to vouch for: those shares stay 0
+    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;  // nothing valid to vouch for: those shares stay 0
     const uint32_t* sm = sums + (uint64_t)it.b * kBatchSumWords + it.node * kSumWords;
     const G1A a = g1_to_affine(load_jac(sm)), bb = g1_to_affine(load_jac(sm + kJacWords));
     const bool w_inf = ct_u[32ull * d.ct + 25] != 0;
@@ -799,7 +795,6 @@ TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_d
                                      coefW + (uint64_t)d.ct * kLineWordsPerPoint, bb.x, fp_neg(bb.y),
                                      !bb.inf && !w_inf);
     batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n);
-    }
 }
 
 TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
@@ -1581,10 +1576,8 @@ TDEC_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_
                                   const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ pk_tbl,
                                   uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t nb = dev_count(nb_dev, cap);  // the batch count is a device word
-    // block-stride over the batches on a resident grid
-    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    if (b >= dev_count(nb_dev, cap)) return;  // grid sized for the bound; the batch count is a device word
     const BatchDesc d = desc[b];
     const uint32_t q = d.start + lane;
     const bool in = q < d.end;
@@ -1660,7 +1653,6 @@ TDEC_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_
         }
         if (lane == 0) store_g2jac(out + kNodeBatch * kSigSumWords + kJacWords, A);
     }
-    }
 }
 
 // e(pk, H) * e(-G1, sig) == 1 with H's lines prepared; sig's lines go to `ls`.
@@ -1674,7 +1666,7 @@ BD bool sig_pair_check(const uint32_t* coefH, const Fp& pkx, const Fp& pky, bool
 // batch, or with `spec` over every batch AND its four 16-groups, item
 // 5b + j, so a small batch count does not pay a separate latency-bound round
 // for the 16-groups); lines: one G2Prepared slot per lane of this launch.
-TDEC_KERNEL void sig_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, uint32_t spec,
+TDEC_KERNEL void sig_batch_check(uint64_t base, uint32_t cap, const uint32_t* __restrict__ n_dev, uint32_t spec,
                                  const CheckItem* __restrict__ items,
                                  const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                  const uint32_t* __restrict__ sums, const uint8_t* __restrict__ leaf_ok,
@@ -1684,8 +1676,9 @@ TDEC_KERNEL void sig_batch_check(uint32_t cap, const uint32_t* __restrict__ n_de
                                  uint32_t* __restrict__ fail_n) {
     // items == null: every batch (count *n_dev), or with `spec` every batch and its 16-groups (5 items each)
     const uint64_t n_items = items ? dev_count(n_dev, cap) : (spec ? 5ull : 1ull) * dev_count(n_dev, cap);
-    uint32_t* my_lines = lines + grid_lane() * kLineWordsPerPoint;  // one G2Prepared slot per resident lane
-    for (uint64_t i = grid_lane(); i < n_items; i += grid_lanes()) {
+    const uint64_t i = base + grid_lane();
+    if (i >= n_items) return;
+    uint32_t* my_lines = lines + grid_lane() * kLineWordsPerPoint;  // one G2Prepared slot per lane of a chunk
     const uint32_t j = (uint32_t)i;
     const CheckItem it = items ? items[j]
                                : (spec ? CheckItem{j / 5u, j % 5u == 0 ? kNodeBatch : kNode16 + j % 5u - 1u}
@@ -1693,26 +1686,25 @@ TDEC_KERNEL void sig_batch_check(uint32_t cap, const uint32_t* __restrict__ n_de
     const BatchDesc d = desc[it.b];
     const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
     const uint32_t l0 = node_first(it.node);
-    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) continue;
+    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;
     const uint32_t* sm = sums + (uint64_t)it.b * kSigBatchSumWords + it.node * kSigSumWords;
     const G1A a = g1_to_affine(load_jac(sm));
     const G2A sg = g2_to_affine(load_g2jac(sm + kJacWords));
     const bool pass = sig_pair_check(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, a.inf, sg, my_lines);
     batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n,
                     spec && !items && it.node == kNodeBatch);
-    }
 }
 
 // Per-share PublicKeyShare::verify with H prepared per document: share
 // sel[base + i] (or base + i), lines: one G2Prepared slot per lane.
-TDEC_KERNEL void sig_verify_shares(uint64_t cap, const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ sel,
+TDEC_KERNEL void sig_verify_shares(uint64_t base, uint64_t cap, const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ sel,
                                    const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_doc,
                                    const uint32_t* __restrict__ share_pk, const uint32_t* __restrict__ pk_aff,
                                    const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ coefH,
                                    uint32_t* __restrict__ lines, uint8_t* __restrict__ ok) {
-    const uint64_t n = dev_count(n_dev, cap);
-    uint32_t* my_lines = lines + grid_lane() * kLineWordsPerPoint;  // one G2Prepared slot per resident lane
-    for (uint64_t i = grid_lane(); i < n; i += grid_lanes()) {
+    const uint64_t i = base + grid_lane();
+    if (i >= dev_count(n_dev, cap)) return;
+    uint32_t* my_lines = lines + grid_lane() * kLineWordsPerPoint;  // one G2Prepared slot per lane of a chunk
     const uint64_t k = sel ? sel[i] : i;
     const uint32_t p = share_pk[k];  // sanitised: an out-of-range pair points at the invalid sentinel key
     G2A sig;
@@ -1723,7 +1715,6 @@ TDEC_KERNEL void sig_verify_shares(uint64_t cap, const uint32_t* __restrict__ n_
                               pa[24] != 0, sig, my_lines);
     }
     ok[k] = good ? 1 : 0;
-    }
 }
 
 // ------------------------------------------------------------------ unit-test hook
@@ -1859,12 +1850,14 @@ hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_
     tdec_pk_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, pk48, pk_aff, pk_status);
     return hipGetLastError();
 }
-// Grid of a grid-stride round over at most `cap` items: one 64-lane block per
-// 64 items up to the resident limit (2 waves per SIMD on 1,024 SIMDs).
-static dim3 resident_grid(uint64_t cap) {
-    const uint64_t b = (cap + 63) / 64;
-    return dim3((uint32_t)(b < kResidentBlocks ? b : kResidentBlocks));
-}
+// Grid of a round over at most `cap` items, one item per lane: lanes past the
+// device-side count return at once.  The TDec kernels handle ONE item per lane
+// (round 1's launch shape, run at 6.4M shares); a grid-stride variant over a
+// resident grid faulted at >= 4M shares, root cause open.
+static dim3 item_grid(uint64_t cap) { return dim3((uint32_t)((cap + 63) / 64)); }
+// Chunks for kernels with a per-lane G2Prepared slot (sig_*): launches of at
+// most kChunkLanes items, the slot indexed by the lane within the chunk.
+constexpr uint64_t kChunkLanes = 64ull * kResidentBlocks;
 
 hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
                                      const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
@@ -1873,7 +1866,7 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
                                      const uint32_t* sel) {
     HBG_COUNT_MARK("tdec_verify_shares", st);
     if (cap == 0) return hipSuccess;
-    tdec_verify_shares<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, share48, share_ct, share_pk, ct_u,
+    tdec_verify_shares<<<item_grid(cap), dim3(64), 0, st>>>(cap, n_dev, share48, share_ct, share_pk, ct_u,
                                                                 ct_status, coefH, coefW, pk_aff, pk_status, ok, sel);
     return hipGetLastError();
 }
@@ -1946,7 +1939,7 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     uint8_t* leaf_ok, hipStream_t st) {
     HBG_COUNT_MARK("tdec_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
-    tdec_batch_leaves<<<dim3(nb_max < kResidentBlocks ? nb_max : kResidentBlocks), dim3(64), 0, st>>>(nb_max, nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
+    tdec_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_max, nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
                                                          pk_aff, pk_status, pk_tbl, sums, leaf_ok);
     return hipGetLastError();
 }
@@ -1967,7 +1960,7 @@ hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const Ch
                                    uint32_t* fail_list, uint32_t* fail_n, hipStream_t st) {
     HBG_COUNT_MARK("tdec_batch_check", st);
     if (cap == 0) return hipSuccess;
-    tdec_batch_check<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, items, desc, perm, sums, leaf_ok, ct_u,
+    tdec_batch_check<<<item_grid(cap), dim3(64), 0, st>>>(cap, n_dev, items, desc, perm, sums, leaf_ok, ct_u,
                                                               coefH, coefW, ok, next, next_n, fail_list, fail_n);
     return hipGetLastError();
 }
@@ -2082,11 +2075,11 @@ hipError_t launch_sig_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint
                                    const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, hipStream_t st) {
     HBG_COUNT_MARK("sig_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
-    sig_batch_leaves<<<dim3(nb_max < kResidentBlocks ? nb_max : kResidentBlocks), dim3(64), 0, st>>>(nb_max, nb_dev, n_doc, desc, perm, share96, share_pk, seeds, pk_aff,
+    sig_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_max, nb_dev, n_doc, desc, perm, share96, share_pk, seeds, pk_aff,
                                                         pk_status, pk_tbl, sums, leaf_ok);
     return hipGetLastError();
 }
-// lines: kResidentBlocks * 64 G2Prepared slots (one per resident lane)
+// lines: kResidentBlocks * 64 G2Prepared slots (one per lane of a launch chunk)
 hipError_t launch_sig_batch_check(uint32_t cap, const uint32_t* n_dev, uint32_t spec, const CheckItem* items,
                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
                                   const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
@@ -2095,9 +2088,14 @@ hipError_t launch_sig_batch_check(uint32_t cap, const uint32_t* n_dev, uint32_t 
     HBG_COUNT_MARK("sig_batch_check", st);
     if (cap == 0) return hipSuccess;
     const uint64_t items_cap = items ? cap : (spec ? 5ull : 1ull) * cap;
-    sig_batch_check<<<resident_grid(items_cap), dim3(64), 0, st>>>(cap, n_dev, spec, items, desc, perm, sums, leaf_ok,
-                                                                   coefH, lines, ok, next, next_n, fail_list, fail_n);
-    return hipGetLastError();
+    for (uint64_t base = 0; base < items_cap; base += kChunkLanes) {
+        const uint64_t m = items_cap - base < kChunkLanes ? items_cap - base : kChunkLanes;
+        sig_batch_check<<<item_grid(m), dim3(64), 0, st>>>(base, cap, n_dev, spec, items, desc, perm, sums, leaf_ok,
+                                                           coefH, lines, ok, next, next_n, fail_list, fail_n);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint32_t* sel, const uint8_t* share96,
                                     const uint32_t* share_doc, const uint32_t* share_pk, const uint32_t* pk_aff,
@@ -2105,9 +2103,14 @@ hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const u
                                     hipStream_t st) {
     HBG_COUNT_MARK("sig_verify_shares", st);
     if (cap == 0) return hipSuccess;
-    sig_verify_shares<<<resident_grid(cap), dim3(64), 0, st>>>(cap, n_dev, sel, share96, share_doc, share_pk, pk_aff,
-                                                               pk_status, coefH, lines, ok);
-    return hipGetLastError();
+    for (uint64_t base = 0; base < cap; base += kChunkLanes) {
+        const uint64_t m = cap - base < kChunkLanes ? cap - base : kChunkLanes;
+        sig_verify_shares<<<item_grid(m), dim3(64), 0, st>>>(base, cap, n_dev, sel, share96, share_doc, share_pk,
+                                                             pk_aff, pk_status, coefH, lines, ok);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace bls
