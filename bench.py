@@ -73,7 +73,11 @@ def parse():
                     help="ciphertexts per TDec step (64 shares each, N=64 t=21; 2.1M shares); 0 disables the "
                          "TDec leg.  Sizes >= 65536 hit an open device fault: DESIGN.md §4")
     ap.add_argument("--epoch-nodes", type=int, default=128,
-                    help="configs[4]: one N-node network spanning all ranks (RCCL all-gather); 0 disables")
+                    help="configs[4]: one N-node HoneyBadger epoch spanning all ranks (RCCL all-gather); 0 disables")
+    ap.add_argument("--epoch-contrib", type=int, default=1 << 20,
+                    help="contribution bytes per node in the configs[4] epoch (threshold-encrypted, then broadcast)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
     ap.add_argument("--wire-msgs", type=int, default=65536,
                     help="SURVEY.md §8(f2): wire messages signed + verified (0 disables)")
     ap.add_argument("--f1-cts", type=int, default=16384,
@@ -540,48 +544,102 @@ def broadcast_wire_leg(ctx, dev, shards, levels, L: int, n_inst: int, reps: int)
             "validate_proofs_per_s": m / (ms_v * 1e-3), "roundtrip_ok": good}
 
 
-def network_leg(ctx, dev, n_nodes: int, reps: int):
-    """configs[4]: the RBC half of one epoch of ONE n_nodes-node network whose
-    nodes are split over all ranks (hydrabadger_amd/network.py): encode the
-    local proposals, one all-gather of shards + Merkle levels (RCCL over xGMI),
-    validate every echo proof, decode all n_nodes proposals.  Timed per phase
-    on every rank, max over ranks."""
+def epoch_leg(ctx, dev, n_nodes: int, contrib: int, reps: int, agg_dev):
+    """configs[4]: one HoneyBadger epoch of ONE n_nodes-node network whose
+    nodes are split over all ranks (hydrabadger_amd/epoch.py): threshold-
+    encrypt every contribution, the Broadcast Value -> Echo -> Ready rounds as
+    bincode wire messages (each round one all-gather, RCCL over xGMI), decode,
+    and ThresholdDecrypt of every accepted ciphertext (shares exchanged by one
+    more all-gather).  Timed per phase on every rank, max over ranks; every
+    contribution must come out of ThresholdDecrypt byte-exact."""
+    from hydrabadger_amd import epoch as hbe
     from hydrabadger_amd import network, shard
     eng = network.DeviceEngine(dev, ctx)
-    ep = network.SpanningEpoch(n_nodes, PAYLOAD, eng)
-    pay = eng.synth_payloads(ep.rank * ep.m, ep.m, PAYLOAD)
-    res = ep.run(pay)  # warm
-    ok = bool((res.status == 1).all().item()) and bool(res.echo_ok.all().item())
-    own = res.payloads[ep.rank * ep.m:(ep.rank + 1) * ep.m, :PAYLOAD]
-    ok = ok and bool(torch.equal(own, pay[:, :PAYLOAD]))
+    ep = hbe.HoneyBadgerEpoch(n_nodes, contrib, eng, seed=1)
+
+    def check(res, e):
+        want = eng.synth(hbe.TAG_CONTRIB, hbe.instance_id(e, 0), n_nodes, contrib)
+        return (bool(res.delivered.all()) and res.accepted == list(range(n_nodes))
+                and bool((res.ct_status == 0).all()) and bool(torch.equal(res.plaintexts, want)))
+    ok = check(ep.run(epoch=0), 0)  # warm
     phases = {}
-    for _ in range(reps):
+    for r in range(reps):
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
-        r = ep.run(pay)
-        for k, v in r.times_ms.items():
+        res = ep.run(epoch=1 + r)
+        ok = ok and check(res, 1 + r)
+        for k, v in res.times_ms.items():
             phases[k] = phases.get(k, 0.0) + v / reps
-    phases = {k: shard.max_over_ranks(v, dev) for k, v in phases.items()}
-    recv = res.exchange_bytes
-    return {"workload": f"one {n_nodes}-node network (RS {ep.N - 2 * ((ep.N - 1) // 3)}+{2 * ((ep.N - 1) // 3)}), "
-                        f"1 MiB proposals, nodes split over {ep.world} rank(s)",
+    phases = {k: shard.max_over_ranks(v, agg_dev) for k, v in phases.items()}
+    f = (n_nodes - 1) // 3
+    return {"workload": f"one {n_nodes}-node HoneyBadger epoch (RS {n_nodes - 2 * f}+{2 * f}, t={f}), "
+                        f"{contrib}-B contributions threshold-encrypted and broadcast, nodes split over "
+                        f"{ep.world} rank(s)",
             "nodes_per_rank": ep.m, "epoch_ms": phases["epoch"], "phases_ms": phases,
-            "proposals_per_s": n_nodes / (phases["epoch"] * 1e-3),
-            "allgather_recv_bytes_per_rank": recv,
-            "allgather_GBps": (recv / (phases["all_gather"] * 1e-3) / 1e9) if recv else None,
-            "all_decoded_ok": ok}
+            "contributions_per_s": n_nodes / (phases["epoch"] * 1e-3),
+            "contribution_GBps": n_nodes * contrib / (phases["epoch"] * 1e-3) / 1e9,
+            "allgather_recv_bytes_per_rank": res.exchange_bytes,
+            "messages_per_epoch": {"value": n_nodes * n_nodes, "echo": n_nodes * n_nodes,
+                                   "ready": n_nodes * n_nodes, "decryption_shares": n_nodes * n_nodes},
+            "all_decrypted_ok": ok}
+
+
+def init_distributed(backend: str, local: int):
+    """One process per GPU: RANK / WORLD_SIZE / MASTER_* from the launcher."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        torch.distributed.init_process_group(backend, **kw)
+    return world, rank
+
+
+def run_timed(step, steps: int, warmup: int, sync, agg_dev) -> float:
+    """W untimed steps, then exactly K steps bracketed by a barrier and a
+    device sync on both sides; the max over ranks of the wall time (s)."""
+    from hydrabadger_amd import shard
+    dist_on = torch.distributed.is_initialized()
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist_on:
+        torch.distributed.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist_on:
+        torch.distributed.barrier()
+    return shard.max_over_ranks(time.perf_counter() - t0, agg_dev)
+
+
+class Legs:
+    """Runs the optional legs after the headline; the first failing leg is
+    recorded in the line (leg_errors) and no further GPU leg runs."""
+
+    def __init__(self):
+        self.errors = {}
+
+    def __call__(self, name, fn):
+        if self.errors:
+            self.errors.setdefault("skipped", []).append(name)
+            return None
+        try:
+            return fn()
+        except Exception as ex:  # reported in the JSON line, never silently dropped
+            self.errors[name] = f"{type(ex).__name__}: {ex}"
+            return None
 
 
 def main():
     a = parse()
     legs = set(LEGS) if a.legs == "all" else set(a.legs.split(","))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
     torch.cuda.set_device(local)
-    if dist:
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank = init_distributed(a.backend, local)
+    dist = world > 1
+    agg_dev = torch.device("cuda", local) if a.backend == "nccl" else torch.device("cpu")
 
     from hydrabadger_amd import _lib, shard
     from hydrabadger_amd import broadcast as bc
@@ -607,19 +665,7 @@ def main():
     def step():
         bc.rbc_encode_merkle_batch(N_NODES, pay, plen, L, shards, levels, ctx=ctx, device=True, asynchronous=True)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    dt = shard.max_over_ranks(time.perf_counter() - t0, dev)
+    dt = run_timed(step, a.steps, a.warmup, torch.cuda.synchronize, agg_dev)
     total_bytes = world * B * PAYLOAD * a.steps
     value = total_bytes / dt / 1e9
 
@@ -648,9 +694,10 @@ def main():
                "rs_encode_traffic_bytes_per_launch": traffic.get("rs_encode_const_22_42"),
                "rs_encode_hbm_GBps": enc_bytes / (ms_encode * 1e-3) / 1e9 if ms_encode > 0 else None}
 
+    run_leg = Legs()
+
     # ---- decode path: reconstruct exactly 2f erasures + tree + glue ----
-    decode = None
-    if not a.no_decode and "decode" in legs:
+    def decode_leg():
         from hydrabadger_amd import workload
         nd = min(B, 2048)
         present = torch.tensor([workload.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
@@ -669,28 +716,26 @@ def main():
         torch.cuda.synchronize()
         ok = bool((st == 1).all().item()) and bool(torch.equal(out[:, :PAYLOAD], pay[:nd]))
         ms_dec = timed(dec, reps)
-        decode = {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
-                  "erased_per_instance": parity, "roundtrip_ok": ok}
+        return {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
+                "erased_per_instance": parity, "roundtrip_ok": ok}
 
-    bwire = None
-    if a.wire_instances > 0 and "bwire" in legs:
-        bwire = broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps)
-
-    epoch = None
-    if a.epoch_nodes > 0 and a.epoch_nodes % world == 0 and "epoch" in legs:
-        epoch = network_leg(ctx, dev, a.epoch_nodes, max(2, min(a.steps, 5)))
-
+    decode = run_leg("decode", decode_leg) if not a.no_decode and "decode" in legs else None
+    bwire = (run_leg("bwire", lambda: broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps))
+             if a.wire_instances > 0 and "bwire" in legs else None)
+    epoch = (run_leg("epoch", lambda: epoch_leg(ctx, dev, a.epoch_nodes, a.epoch_contrib, max(2, min(a.steps, 5)),
+                                                agg_dev))
+             if a.epoch_nodes > 0 and a.epoch_nodes % world == 0 and "epoch" in legs else None)
     tdec = tdec_ep = None
     if a.tdec_cts > 0 and "tdec" in legs:
-        tdec, tdec_ep = tdec_leg(ctx, dev, a.tdec_cts, 2, seed=1 + rank)
-        tdec["value"] = shard.sum_over_ranks(tdec["value"], dev)  # whole-job shares/s
-
-    wire = tdec_in = None
-    if a.wire_msgs > 0 and "wire" in legs:
-        wire = wire_leg(ctx, dev, a.wire_msgs, 256, 2)
-    if a.f1_cts > 0 and "f1" in legs:
-        tdec_in = tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2)
-    coin = coin_leg(ctx, dev, a.coins, N_NODES, 2) if a.coins > 0 and "coin" in legs else None
+        r = run_leg("tdec", lambda: tdec_leg(ctx, dev, a.tdec_cts, 2, seed=1 + rank))
+        if r is not None:
+            tdec, tdec_ep = r
+            tdec["value"] = shard.sum_over_ranks(tdec["value"], agg_dev)  # whole-job shares/s
+    wire = run_leg("wire", lambda: wire_leg(ctx, dev, a.wire_msgs, 256, 2)) if a.wire_msgs > 0 and "wire" in legs \
+        else None
+    tdec_in = (run_leg("f1", lambda: tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2))
+               if a.f1_cts > 0 and "f1" in legs else None)
+    coin = run_leg("coin", lambda: coin_leg(ctx, dev, a.coins, N_NODES, 2)) if a.coins > 0 and "coin" in legs else None
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -716,6 +761,7 @@ def main():
             "wire_signatures": wire,
             "tdec_inputs": tdec_in,
             "coin": coin,
+            "leg_errors": run_leg.errors or None,
         }
         print(json.dumps(line), flush=True)
     ctx.close()

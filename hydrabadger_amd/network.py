@@ -39,6 +39,7 @@ import torch.distributed as dist
 
 from . import _lib, workload
 from . import broadcast as bc
+from .tdec_workload import G1_GENERATOR
 
 
 def proof_index_map(n: int) -> tuple[np.ndarray, np.ndarray]:
@@ -62,6 +63,17 @@ def proof_index_map(n: int) -> tuple[np.ndarray, np.ndarray]:
             li //= 2
         nd[j] = k
     return idx, nd
+
+
+def all_gather_rows(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """Rank-major concatenation of every rank's equally shaped tensor along
+    dim 0: one all_gather_into_tensor (RCCL over xGMI with backend "nccl"; the
+    same call under gloo in the CPU rehearsals)."""
+    if world == 1:
+        return t
+    out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
 
 
 def arrival_mask(instance: int, n: int, epoch: int = 0) -> list:
@@ -140,6 +152,79 @@ class DeviceEngine:
                             asynchronous=True)
         return out, plen, st
 
+    # ---- the HoneyBadger epoch's primitives (hydrabadger_amd/epoch.py) ----
+    def _flags(self):
+        return _lib.HBG_DEVICE | _lib.HBG_ASYNC
+
+    def synth(self, tag: int, first: int, m: int, nbytes: int):
+        out = self.zeros((m, max(nbytes, 1)))
+        bc.synth_bytes(tag, first, nbytes, out, ctx=self.ctx, device=True)
+        return out[:, :nbytes]
+
+    def key_points(self, sk32):
+        """[s] G1 for each 32-byte scalar (public keys / key shares):
+        decrypt_share_no_verify with U = the G1 generator."""
+        k = sk32.shape[0]
+        g1 = torch.from_numpy(np.frombuffer(G1_GENERATOR, np.uint8).copy()).to(self.device)
+        i32 = dict(dtype=torch.int32, device=self.device)
+        return self.decrypt_shares(g1.view(1, 48), sk32, torch.zeros(k, **i32), torch.arange(k, **i32))
+
+    def encrypt(self, pk48, msgs, r32):
+        m, P = msgs.shape
+        off = torch.arange(m + 1, dtype=torch.int64, device=self.device) * P
+        U, W = self.zeros((m, 48)), self.zeros((m, 96))
+        V = self.zeros((max(m * P, 1),))
+        _lib.check(_lib.lib().hbg_tdec_encrypt(self.ctx.h, pk48.contiguous().data_ptr(), m, r32.contiguous().data_ptr(),
+                                               msgs.contiguous().data_ptr(), off.data_ptr(), U.data_ptr(), V.data_ptr(),
+                                               W.data_ptr(), self._flags()), "encrypt_with_rng")
+        return U, V[:m * P].view(m, P), W
+
+    def write_proof_msgs(self, n_nodes: int, L: int, shards, levels, tag: int, inst, index, off):
+        out = self.zeros((max(int(off[-1]), 1),))
+        bc.write_proof_msgs_batch(n_nodes, L, shards, levels, tag, inst, index, out,
+                                  torch.from_numpy(off).to(self.device), ctx=self.ctx, device=True, asynchronous=True)
+        return out[:int(off[-1])]
+
+    def read_msgs(self, n_nodes: int, L: int, buf, off):
+        M = off.shape[0] - 1
+        S = (max(L, 1) + 15) // 16 * 16
+        depth = max(_lib.merkle_depth(n_nodes), 1)
+        i32 = dict(dtype=torch.int32, device=self.device)
+        tag, index, nd, st = (torch.zeros(M, **i32) for _ in range(4))
+        vals, dig, roots = self.zeros((M, S)), self.zeros((M, depth, 32)), self.zeros((M, 32))
+        bc.read_msgs_batch(n_nodes, L, buf, torch.from_numpy(off).to(self.device), tag, vals, index, dig, nd, roots,
+                           st, ctx=self.ctx, device=True, asynchronous=True)
+        return tag, vals, index, dig, nd, roots, st
+
+    def validate_table(self, n_nodes: int, L: int, vals, index, dig, nd, roots):
+        M = vals.shape[0]
+        ok = self.zeros((M,))
+        _lib.check(_lib.lib().hbg_merkle_validate(self.ctx.h, n_nodes, L, vals.data_ptr(), vals.shape[-1],
+                                                  index.data_ptr(), dig.data_ptr(), nd.data_ptr(), roots.data_ptr(),
+                                                  ok.data_ptr(), M, self._flags()), "Proof::validate")
+        return ok
+
+    def decrypt_shares(self, U48, sk32, pair_ct, pair_sk):
+        n = pair_ct.shape[0]
+        out = self.zeros((max(n, 1), 48))
+        st = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
+        _lib.check(_lib.lib().hbg_tdec_decrypt_shares(self.ctx.h, U48.shape[0], U48.contiguous().data_ptr(),
+                                                      sk32.shape[0], sk32.contiguous().data_ptr(), n,
+                                                      pair_ct.data_ptr(), pair_sk.data_ptr(), out.data_ptr(),
+                                                      st.data_ptr(), self._flags()), "decrypt_share_no_verify")
+        return out[:n]
+
+    def threshold_decrypt(self, t: int, n_nodes: int, U, V, V_off, W, pk48, share48, arrival):
+        n_ct = U.shape[0]
+        pt = self.zeros((max(int(V.numel()), 1),))
+        st = torch.zeros(n_ct, dtype=torch.int32, device=self.device)
+        oc = self.zeros((n_ct, n_nodes))
+        from . import threshold as th
+        th.threshold_decrypt_arrays(t, n_nodes, U.contiguous(), V.contiguous(), V_off, W.contiguous(),
+                                    pk48.contiguous(), share48.contiguous(), arrival, pt, st, oc, ctx=self.ctx,
+                                    device=True, asynchronous=True)
+        return pt[:V.numel()], st, oc
+
     def sync(self):
         torch.cuda.synchronize(self.device)
 
@@ -173,12 +258,7 @@ class SpanningEpoch:
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return t
-        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        if dist.get_backend(self.group) == "gloo":
-            dist.all_gather(list(out.chunk(self.world)), t.contiguous(), group=self.group)
-        else:
-            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out
+        return all_gather_rows(t, self.world, self.group)
 
     def run(self, payloads, epoch: int = 0) -> EpochResult:
         """payloads: [m][PS] u8 — this rank's nodes' proposals (engine tensors)."""

@@ -1,0 +1,173 @@
+"""SURVEY.md §8 f4 + a18: one HoneyBadger epoch (hydrabadger_amd/epoch.py)
+against oracle/epoch.py, the node-by-node restatement of hbbft's Broadcast
+(Value -> Echo -> Ready with the N-f / 2f+1 / N-2f thresholds) and
+ThresholdDecrypt over the wire-format messages.
+
+CPU: the product orchestration with the oracle-backed engine, world 1 and
+gloo world 2 (the all_gather_into_tensor branch RCCL takes), honest and with
+faulty nodes.  GPU: the same epochs through DeviceEngine on cuda:0.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hydrabadger_amd import epoch as hbe
+from oracle import epoch as oep
+from oracle import synth
+
+FAULTS = {
+    "honest": {},
+    # a crashed node, a Value corrupted for one recipient, a node echoing garbage,
+    # a node sending shares made with another node's key, a corrupted ciphertext
+    "faulty": dict(silent={3}, bad_value={(0, 1)}, bad_echo={2}, bad_share={5}, bad_ct={6}),
+}
+
+
+def _faults(spec, mod):
+    return mod.Faults(**{k: frozenset(v) for k, v in spec.items()})
+
+
+def _np(t):
+    return t.cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+def compare(res: hbe.EpochResult, exp: oep.EpochOut, P: int):
+    """Bit-exact agreement of the batched epoch with the node-by-node oracle."""
+    N = len(exp.delivered)
+    assert _np(res.value_ok).astype(bool).tolist() == exp.value_ok
+    assert _np(res.echo_ok).astype(bool).tolist() == exp.echo_ok
+    assert _np(res.echo_count).tolist() == exp.echo_count
+    assert _np(res.ready_count).tolist() == exp.ready_count
+    assert _np(res.delivered).astype(bool).tolist() == exp.delivered
+    pays = _np(res.payloads)
+    C = hbe.ct_bytes(P)
+    for p in range(N):
+        if exp.payloads[p] is not None:
+            assert pays[p, :C].tobytes() == exp.payloads[p], p
+    assert res.accepted == exp.accepted
+    assert _np(res.ct_status).tolist() == exp.ct_status
+    pts = _np(res.plaintexts)
+    for q, pt in enumerate(exp.plaintexts):
+        if pt is not None:
+            assert pts[q].tobytes() == pt, q
+    assert _np(res.share_outcome).tolist() == exp.share_outcome
+
+
+# ----------------------------------------------------------------------------- oracle sanity
+def test_oracle_epoch_honest_delivers_every_contribution():
+    N, P = 4, 40
+    out = oep.run_epoch(N, P, seed=3)
+    assert out.delivered == [True] * N and out.accepted == list(range(N))
+    assert out.ct_status == [0] * N
+    for p in range(N):
+        assert out.plaintexts[p] == synth.synth_bytes(oep.TAG_CONTRIB, oep.instance_id(0, p), P)
+    f = (N - 1) // 3
+    for oc in out.share_outcome:  # exactly t+1 = f+1 accepted, the rest ignored
+        assert oc.count(1) == f + 1 and oc.count(3) == N - f - 1
+
+
+def test_oracle_epoch_fault_semantics():
+    N, P = 7, 24
+    out = oep.run_epoch(N, P, seed=2, faults=_faults(FAULTS["faulty"], oep))
+    assert not out.value_ok[0][1]                    # the corrupted Value fails its proof
+    assert not any(out.echo_ok[2])                   # node 2's echoes all fail
+    assert not any(out.echo_ok[3])                   # the silent node echoes nothing
+    assert not out.delivered[3]                      # ... and proposes nothing
+    k6 = out.accepted.index(6)
+    assert out.ct_status[k6] == oep.T.E_INVALID_CIPHERTEXT
+    for q, p in enumerate(out.accepted):
+        if p != 6:
+            assert out.ct_status[q] == 0
+            assert out.share_outcome[q][3] == 0      # silent: no share
+            assert out.share_outcome[q][5] in (0, 2, 3)  # bad share: fault if processed, never accepted
+
+
+# ----------------------------------------------------------------------------- product orchestration on CPU
+@pytest.mark.parametrize("name,N,P", [("honest", 4, 40), ("faulty", 7, 24)])
+def test_epoch_world1_oracle_engine(name, N, P):
+    from tests.oracle_engine import OracleEngine
+    ep = hbe.HoneyBadgerEpoch(N, P, OracleEngine(), seed=2)
+    res = ep.run(epoch=1, faults=_faults(FAULTS[name], hbe))
+    compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep)), P)
+    assert res.exchange_bytes == 0
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, q, N, P, name):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.oracle_engine import OracleEngine
+        res = hbe.HoneyBadgerEpoch(N, P, OracleEngine(), seed=2).run(epoch=1, faults=_faults(FAULTS[name], hbe))
+        # tensors -> numpy: a queued tensor is shared through a handle that dies with this process
+        plain = {k: (v.numpy().copy() if isinstance(v, torch.Tensor) else v) for k, v in vars(res).items()}
+        q.put((rank, hbe.EpochResult(**plain)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,N,P", [("honest", 4, 40), ("faulty", 8, 24)])
+def test_epoch_gloo_world2(name, N, P):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, N, P, name)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=600) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep))
+    for r in range(2):
+        compare(got[r], exp, P)
+        assert got[r].exchange_bytes > 0
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,N,P", [("honest", 4, 40), ("faulty", 7, 24), ("faulty", 16, 300)])
+def test_epoch_device_world1(name, N, P):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import network
+    eng = network.DeviceEngine(torch.device("cuda:0"))
+    try:
+        res = hbe.HoneyBadgerEpoch(N, P, eng, seed=2).run(epoch=1, faults=_faults(FAULTS[name], hbe))
+        compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep)), P)
+    finally:
+        eng.ctx.close()
+
+
+@pytest.mark.gpu
+def test_epoch_device_n64_honest_plaintexts():
+    """configs[3]/[4] shape: N=64, every contribution decrypted to its bytes
+    (size-independent property: no oracle epoch at this size)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import network
+    eng = network.DeviceEngine(torch.device("cuda:0"))
+    try:
+        N, P = 64, 4096
+        res = hbe.HoneyBadgerEpoch(N, P, eng, seed=5).run(epoch=2)
+        assert bool(res.delivered.all()) and res.accepted == list(range(N))
+        assert _np(res.ct_status).tolist() == [0] * N
+        pts = _np(res.plaintexts)
+        for p in (0, 31, 63):
+            assert pts[p].tobytes() == synth.synth_bytes(hbe.TAG_CONTRIB, hbe.instance_id(2, p), P)
+        oc = _np(res.share_outcome)
+        assert ((oc == 1).sum(1) == 22).all() and ((oc == 3).sum(1) == N - 22).all()
+    finally:
+        eng.ctx.close()
