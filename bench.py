@@ -59,7 +59,7 @@ def merkle_alg(N: int, L: int):
     return ops, bytes_
 
 
-LEGS = ("rbc", "decode", "bwire", "epoch", "tdec", "wire", "f1", "coin")
+LEGS = ("rbc", "decode", "cfg1", "n128", "bwire", "epoch", "tdec", "wire", "f1", "coin")
 
 
 def parse():
@@ -86,6 +86,10 @@ def parse():
                     help="SURVEY.md §8(f3): common coins (x64 signature shares) signed, verified, combined (0 disables)")
     ap.add_argument("--wire-instances", type=int, default=1024,
                     help="SURVEY.md §8(f4): instances whose N Value messages are written/parsed/validated (0 disables)")
+    ap.add_argument("--cfg1-instances", type=int, default=10000,
+                    help="configs[1] leg: N=16 f=5 64 KiB instances (encode+Merkle+decode); 0 disables")
+    ap.add_argument("--n128-instances", type=int, default=2048,
+                    help="N=128 (RS 44+84) 1 MiB encode+Merkle+decode instances; 0 disables")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--legs", default="all",
@@ -489,6 +493,60 @@ def coin_leg(ctx, dev, n_coins: int, n_nodes: int, reps: int):
             "heads_fraction": float(par.float().mean().item()), "all_ok": good}
 
 
+def rbc_config_leg(ctx, dev, n_nodes: int, payload: int, n_inst: int, reps: int, config: str):
+    """encode+Merkle (send_shards) and decode (2f erasures) throughput of one
+    RBC configuration at batch size, with the VALU fraction of its
+    merkle_build launch (the same algorithmic count as the headline) and the
+    decode round trip checked."""
+    from hydrabadger_amd import _lib, workload
+    from hydrabadger_amd import broadcast as bc
+    L = _lib.shard_len(n_nodes, payload)
+    S = (L + 15) // 16 * 16
+    nodes = _lib.merkle_nodes(n_nodes)
+    data, parity = bc.shard_counts(n_nodes)
+    PS = (payload + 15) // 16 * 16
+    pay = torch.zeros((n_inst, PS), dtype=torch.uint8, device=dev)
+    bc.synth_bytes(1, 0x10000000, payload, pay, ctx=ctx, device=True)
+    plen = torch.full((n_inst,), payload, dtype=torch.int64, device=dev)
+    shards = torch.empty((n_inst, n_nodes, S), dtype=torch.uint8, device=dev)
+    levels = torch.empty((n_inst, nodes, 32), dtype=torch.uint8, device=dev)
+
+    def enc():
+        bc.rbc_encode_merkle_batch(n_nodes, pay, plen, L, shards, levels, ctx=ctx, device=True, asynchronous=True)
+
+    def mk():
+        bc.merkle_build_batch(n_nodes, L, shards, levels, ctx=ctx, device=True, asynchronous=True)
+    enc()
+    ms_step = timed(enc, reps)
+    ms_merkle = timed(mk, reps)
+    present = torch.tensor([workload.erasure_mask(0x10000000 + k, n_nodes, parity) for k in range(n_inst)],
+                           dtype=torch.uint8, device=dev)
+    roots = levels[:, nodes - 1, :].contiguous()
+    OS = (data * L + 15) // 16 * 16
+    out = torch.empty((n_inst, OS), dtype=torch.uint8, device=dev)
+    dplen = torch.empty(n_inst, dtype=torch.int64, device=dev)
+    st = torch.empty(n_inst, dtype=torch.uint8, device=dev)
+    work = shards.clone()
+
+    def dec():
+        bc.rbc_decode_batch(n_nodes, L, work, present, roots, out, dplen, st, ctx=ctx, device=True,
+                            asynchronous=True)
+    dec()
+    torch.cuda.synchronize()
+    ok = bool((st == 1).all().item()) and bool(torch.equal(out[:, :payload], pay[:, :payload]))
+    ms_dec = timed(dec, reps)
+    ops, _ = merkle_alg(n_nodes, L)
+    achieved = ops * n_inst / (ms_merkle * 1e-3)
+    return {"config": config, "n_nodes": n_nodes, "f": (n_nodes - 1) // 3, "rs": f"{data}+{parity}",
+            "payload_bytes": payload, "shard_len": L, "instances": n_inst,
+            "encode_merkle_GBps": n_inst * payload / (ms_step * 1e-3) / 1e9, "encode_merkle_ms": ms_step,
+            "merkle_build_ms": ms_merkle, "rs_encode_ms": max(ms_step - ms_merkle, 0.0),
+            "merkle_valu": {"achieved": achieved / 1e12, "peak": VALU_PEAK / 1e12, "frac": achieved / VALU_PEAK,
+                            "unit": "T int32 lane-ops/s", "alg_ops_per_instance": ops},
+            "decode_GBps": n_inst * payload / (ms_dec * 1e-3) / 1e9, "decode_ms": ms_dec,
+            "erased_per_instance": parity, "roundtrip_ok": ok}
+
+
 def broadcast_wire_leg(ctx, dev, shards, levels, L: int, n_inst: int, reps: int):
     """SURVEY.md §8(f4): every Value message (bincode Message::Value(proof(i)))
     of n_inst encoded N=64 instances written from the shard batch + levels,
@@ -720,6 +778,12 @@ def main():
                 "erased_per_instance": parity, "roundtrip_ok": ok}
 
     decode = run_leg("decode", decode_leg) if not a.no_decode and "decode" in legs else None
+    cfg1 = (run_leg("cfg1", lambda: rbc_config_leg(ctx, dev, 16, 1 << 16, a.cfg1_instances, reps,
+                                                   "BASELINE.json configs[1]: N=16 f=5, 64 KiB proposals"))
+            if a.cfg1_instances > 0 and "cfg1" in legs else None)
+    n128 = (run_leg("n128", lambda: rbc_config_leg(ctx, dev, 128, PAYLOAD, a.n128_instances, reps,
+                                                   "BASELINE.json configs[4] coding: N=128 f=42, 1 MiB proposals"))
+            if a.n128_instances > 0 and "n128" in legs else None)
     bwire = (run_leg("bwire", lambda: broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps))
              if a.wire_instances > 0 and "bwire" in legs else None)
     epoch = (run_leg("epoch", lambda: epoch_leg(ctx, dev, a.epoch_nodes, a.epoch_contrib, max(2, min(a.steps, 5)),
@@ -756,6 +820,8 @@ def main():
             "roofline": roofline, "kernels": kernels, "decode": decode, "cpu_baseline": cpu,
             "shard_bytes_GBps": value * N_NODES * L / PAYLOAD,
             "tdec": tdec,
+            "config1_n16": cfg1,
+            "n128_encode_merkle": n128,
             "network_epoch": epoch,
             "broadcast_wire": bwire,
             "wire_signatures": wire,

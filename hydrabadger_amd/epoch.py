@@ -255,7 +255,7 @@ class HoneyBadgerEpoch:
         rall = self._gather(rbuf.view(m * N, 36)).view(-1)
         rsent_all = self._gather(rsent)                       # [N j][N p]
         r_off = np.arange(N * N + 1, dtype=np.int64) * 36
-        tag, _, _, _, _, rroots, st = e.read_msgs(N, L, rall, r_off)
+        tag, _, _, _, _, rroots, st = e.read_msgs(N, 16, rall, r_off)   # digests only: no value table needed
         rgood = (st == 0) & (tag == _lib.HBG_MSG_READY)
         rmatch = (rroots.view(N, N, 32) == root_p.unsqueeze(0)).all(-1) & rgood.view(N, N) & (rsent_all == 1)
         ready_count = rmatch.sum(0)                           # [p]
