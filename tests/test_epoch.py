@@ -171,3 +171,14 @@ def test_epoch_device_n64_honest_plaintexts():
         assert ((oc == 1).sum(1) == 22).all() and ((oc == 3).sum(1) == N - 22).all()
     finally:
         eng.ctx.close()
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 5])
+@pytest.mark.parametrize("spec", [{}, {"silent": {0}}, {"bad_share": {1}, "bad_echo": {0}}])
+def test_epoch_small_networks_oracle_engine(N, spec):
+    """Trivial coding (N <= 3: no parity), a single node, and crashed / faulty
+    nodes in networks too small to tolerate them: same outcome as the oracle."""
+    from tests.oracle_engine import OracleEngine
+    spec = {k: {x % N for x in v} for k, v in spec.items()}
+    res = hbe.HoneyBadgerEpoch(N, 17, OracleEngine(), seed=4).run(epoch=3, faults=_faults(spec, hbe))
+    compare(res, oep.run_epoch(N, 17, seed=4, epoch=3, faults=_faults(spec, oep)), 17)
