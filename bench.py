@@ -171,6 +171,21 @@ def fp_count_profile(n_nodes: int, t: int, bad_rate: float) -> dict:
     return d
 
 
+# Kernels whose Fp work is per call (the N public-key shares), not per share:
+# their profiled count is re-spread over this run's share count.
+FP_FIXED_PER_CALL = ("tdec_pk_table", "tdec_pk_prepare")
+
+
+def fp_per_share(prof: dict, key: str, n_shares: int) -> float:
+    """Fp multiplications per share at n_shares from the profile's per-kernel
+    counts (per-share and per-ciphertext kernels scale with the shares; the
+    per-call key-table work is divided by this run's share count)."""
+    total = 0.0
+    for name, v in prof[key].items():
+        total += (v["fp_mul"] + v["fp_sqr"]) / n_shares if name in FP_FIXED_PER_CALL else v["per_share"]
+    return total
+
+
 def kernel_meta(names) -> dict:
     """VGPR / scratch / waves-per-SIMD of the named kernels (tools/kernel_meta.py)."""
     try:
@@ -282,9 +297,9 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
                      f"{bad_rate:.0%} replaced (three kinds); generated in {t_gen:.1f} s, HBM-resident"}
     prof = fp_count_profile(N, t, bad_rate)
     if prof:
-        per_share = prof["per_share_total"]
+        per_share = fp_per_share(prof, "kernels", n)
         achieved = per_share * MADS_PER_FP_MUL * n / (ms * 1e-3)
-        per_share_v = prof.get("per_share_verify_total", per_share)
+        per_share_v = fp_per_share(prof, "verify_kernels", n)
         achieved_v = per_share_v * MADS_PER_FP_MUL * n / (ms_v * 1e-3)
         out["roofline"] = {
             "kernel": "hbg_tdec_threshold_decrypt (all its kernels; per-kernel counts in the profile)",
