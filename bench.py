@@ -690,16 +690,14 @@ def run_timed(step, steps: int, warmup: int, sync, agg_dev) -> float:
 
 
 class Legs:
-    """Runs the optional legs after the headline; the first failing leg is
-    recorded in the line (leg_errors) and no further GPU leg runs."""
+    """Runs the optional legs after the headline; a failing leg is recorded in
+    the line (leg_errors) and the others still run (after a device fault they
+    fail fast with their own HIP errors, which are recorded too)."""
 
     def __init__(self):
         self.errors = {}
 
     def __call__(self, name, fn):
-        if self.errors:
-            self.errors.setdefault("skipped", []).append(name)
-            return None
         try:
             return fn()
         except Exception as ex:  # reported in the JSON line, never silently dropped
@@ -795,28 +793,31 @@ def main():
                 "erased_per_instance": parity, "roundtrip_ok": ok}
 
     decode = run_leg("decode", decode_leg) if not a.no_decode and "decode" in legs else None
+    bwire = (run_leg("bwire", lambda: broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps))
+             if a.wire_instances > 0 and "bwire" in legs else None)
+    wire = run_leg("wire", lambda: wire_leg(ctx, dev, a.wire_msgs, 256, 2)) if a.wire_msgs > 0 and "wire" in legs \
+        else None
+    tdec_in = (run_leg("f1", lambda: tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2))
+               if a.f1_cts > 0 and "f1" in legs else None)
+    coin = run_leg("coin", lambda: coin_leg(ctx, dev, a.coins, N_NODES, 2)) if a.coins > 0 and "coin" in legs else None
+
+    # the legs added this round run last (the full epoch last of all): a failure there cannot cost the others
     cfg1 = (run_leg("cfg1", lambda: rbc_config_leg(ctx, dev, 16, 1 << 16, a.cfg1_instances, reps,
                                                    "BASELINE.json configs[1]: N=16 f=5, 64 KiB proposals"))
             if a.cfg1_instances > 0 and "cfg1" in legs else None)
     n128 = (run_leg("n128", lambda: rbc_config_leg(ctx, dev, 128, PAYLOAD, a.n128_instances, reps,
                                                    "BASELINE.json configs[4] coding: N=128 f=42, 1 MiB proposals"))
             if a.n128_instances > 0 and "n128" in legs else None)
-    bwire = (run_leg("bwire", lambda: broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps))
-             if a.wire_instances > 0 and "bwire" in legs else None)
-    epoch = (run_leg("epoch", lambda: epoch_leg(ctx, dev, a.epoch_nodes, a.epoch_contrib, max(2, min(a.steps, 5)),
-                                                agg_dev))
-             if a.epoch_nodes > 0 and a.epoch_nodes % world == 0 and "epoch" in legs else None)
     tdec = tdec_ep = None
     if a.tdec_cts > 0 and "tdec" in legs:
         r = run_leg("tdec", lambda: tdec_leg(ctx, dev, a.tdec_cts, 2, seed=1 + rank))
         if r is not None:
             tdec, tdec_ep = r
             tdec["value"] = shard.sum_over_ranks(tdec["value"], agg_dev)  # whole-job shares/s
-    wire = run_leg("wire", lambda: wire_leg(ctx, dev, a.wire_msgs, 256, 2)) if a.wire_msgs > 0 and "wire" in legs \
-        else None
-    tdec_in = (run_leg("f1", lambda: tdec_inputs_leg(ctx, dev, a.f1_cts, N_NODES, 2))
-               if a.f1_cts > 0 and "f1" in legs else None)
-    coin = run_leg("coin", lambda: coin_leg(ctx, dev, a.coins, N_NODES, 2)) if a.coins > 0 and "coin" in legs else None
+
+    epoch = (run_leg("epoch", lambda: epoch_leg(ctx, dev, a.epoch_nodes, a.epoch_contrib, max(2, min(a.steps, 5)),
+                                                agg_dev))
+             if a.epoch_nodes > 0 and a.epoch_nodes % world == 0 and "epoch" in legs else None)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
