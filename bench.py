@@ -824,7 +824,7 @@ def main():
         if "rbc" in legs:
             cpu = cpu_baseline(a.cpu_sample)
         if tdec is not None:
-            tdec["cpu_baseline"] = cpu_baseline_tdec(tdec_ep)
+            tdec["cpu_baseline"] = run_leg("tdec_cpu_baseline", lambda: cpu_baseline_tdec(tdec_ep))
 
     if rank == 0:
         line = {
