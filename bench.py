@@ -69,9 +69,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--instances", type=int, default=8192, help="1 MiB proposals per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="instances in the CPU-baseline sample")
-    ap.add_argument("--tdec-cts", type=int, default=32768,
-                    help="ciphertexts per TDec step (64 shares each, N=64 t=21; 2.1M shares); 0 disables the "
-                         "TDec leg.  Sizes >= 65536 hit an open device fault: DESIGN.md §4")
+    ap.add_argument("--tdec-cts", type=int, default=100000,
+                    help="ciphertexts per TDec step (BASELINE.json configs[3]: 100k x 64 shares, N=64 t=21); "
+                         "0 disables the TDec leg")
     ap.add_argument("--epoch-nodes", type=int, default=128,
                     help="configs[4]: one N-node HoneyBadger epoch spanning all ranks (RCCL all-gather); 0 disables")
     ap.add_argument("--epoch-contrib", type=int, default=4096,
