@@ -91,6 +91,7 @@ SIGNATURES = {
     "hbg_sig_verify_shares": (_i, [_vp, _u32, _u8p, _vp, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_test_bls": (_i, [_vp, C.c_int, _u32, _vp, _u32, _vp, _u32]),
     "hbg_test_set_tdec_batched": (_i, [_vp, C.c_int]),
+    "hbg_test_set_rbc_fused": (_i, [_vp, C.c_int]),
 }
 
 _lib = None

@@ -46,6 +46,8 @@ struct hbg_ctx {
     // (pk fixed-base tables when each key verifies >= kPkTableMinUses shares), 2 batched + tables always
     // (and, for signature shares, no speculative 16-group round)
     int tdec_batched = 1;
+    // hbg_rbc_encode_merkle schedule (hbg_test_set_rbc_fused): 0 rs_encode_const + merkle_build, 1 fused
+    int rbc_fused = 0;
     int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
     std::mutex mu;
 };
@@ -196,7 +198,7 @@ int finish(hbg_ctx* c, uint32_t flags) {
 // Encode parity for n instances on a device buffer with row stride S.
 int encode_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t S, uint64_t n,
                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen) {
-    if (has_const_encoder(D, Q)) {
+    if (const_encoder_fits(D, Q, S, payloads ? pstride : 0, false)) {
         HBG_TRY(launch_rs_encode_const(D, Q, shards, S, L, n, payloads, pstride, plen, c->stream));
         return HBG_OK;
     }
@@ -452,6 +454,10 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
     auto run = [&](const uint8_t* dpay, uint64_t dps, const uint64_t* dplen, uint8_t* dsh, uint64_t S,
                    uint8_t* dlev) -> int {
         HBG_TRY(launch_rbc_check_plen(n, dplen, dps, D, L, c->d_err, c->stream));
+        if (c->rbc_fused && Q && const_encoder_fits(D, Q, S, dps, true)) {  // one launch: encode + leaves + tree
+            HBG_TRY(launch_rbc_encode_merkle(D, Q, dsh, S, L, n, dpay, dps, dplen, dlev, c->stream));
+            return HBG_OK;
+        }
         if (Q) {
             HBG_CHECK(encode_device(c, D, Q, L, dsh, S, n, dpay, dps, dplen));
         } else {
@@ -1179,6 +1185,14 @@ int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
     std::lock_guard<std::mutex> g(c->mu);
     if (on < 0 || on > 2) return HBG_E_ARG;
     c->tdec_batched = on;
+    return HBG_OK;
+}
+
+int hbg_test_set_rbc_fused(hbg_ctx* c, int on) {
+    if (!c) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (on < 0 || on > 1) return HBG_E_ARG;
+    c->rbc_fused = on;
     return HBG_OK;
 }
 

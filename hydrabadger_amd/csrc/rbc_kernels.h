@@ -67,8 +67,14 @@ inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
 }
 
 bool has_const_encoder(uint32_t D, uint32_t Q);
+bool const_encoder_fits(uint32_t D, uint32_t Q, uint64_t S, uint64_t pstride, bool fused);
 hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
+// Fused send_shards (prefix/pad/chunk + Coding::encode + MerkleTree::from_vec)
+// for the (D, Q) with a compile-time coding matrix (has_const_encoder).
+hipError_t launch_rbc_encode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                    const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, uint8_t* levels,
+                                    hipStream_t st);
 hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,
                             const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
 hipError_t launch_rbc_check_plen(uint64_t n, const uint64_t* plen, uint64_t pstride, uint32_t D, uint64_t L,

@@ -59,47 +59,79 @@ __device__ __forceinline__ void mac_column(uint32_t (&acc)[Q], const NibPair& T,
 // payload, so the address is a wave-uniform row base + p and the byte shift
 // (J*L mod 4) is uniform: one dwordx2 load + v_alignbyte per word, no
 // per-lane branches.  Loads run kPrefetch columns ahead of the arithmetic.
+// 3 as 2 with the D windows loaded by the caller ahead of time (the fused
+// kernel issues a pass's loads during the previous pass's Keccak work).
 typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 #ifndef HBG_ENC_PREFETCH
 #define HBG_ENC_PREFETCH 6
 #endif
 constexpr int kPrefetch = HBG_ENC_PREFETCH;
 
+// Raw buffer resource over [p, p + 2^31): loads/stores through it take the
+// uniform row offset in an SGPR (soffset) and the lane's offset in a VGPR, so
+// the encoder keeps no per-row 64-bit VGPR address.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+constexpr int kBufSc1 = 16;  // buffer aux bit: sc1 (served by L2, not the CU's vector L1)
+
+// The rows of one encode: shard rows through `sh` (row J of the instance at
+// byte J*S + vsh of the resource; vsh = the lane's instance offset + 4t) and
+// the payload through `py` (value byte v of the instance at byte v - 4 +
+// vpy).  p0 (wave-uniform) + t is the column: its 4 bytes at 4(p0 + t).
+struct EncodeRows {
+    __amdgpu_buffer_rsrc_t sh, py;
+    uint32_t vsh, vpy;
+    uint64_t S, L;
+    uint32_t p0, t;
+    uint8_t* __restrict__ base;       // MODE 1 only: this lane's instance rows
+    const uint8_t* __restrict__ pay;  // MODE 1 only: this lane's payload
+    uint64_t P;
+    const u32x2_a4* pre;              // MODE 3 only: the D payload windows, loaded ahead (payload_window)
+};
+
+// MODE 2's payload window of data row J at column p0 + t (8 bytes at the
+// 4-aligned payload byte below value byte J*L + 4p): a buffer load.
+template <int J>
+__device__ __forceinline__ u32x2_a4 payload_window(const EncodeRows& r, uint32_t p0) {
+    const uint32_t so = (uint32_t)(((uint64_t)J * r.L + 4 * (uint64_t)p0 - 4) & ~3ull);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.py, r.vpy, so, 0);
+    return u32x2_a4{v[0], v[1]};
+}
+
 template <int D, int Q, int MODE>
 struct EncodeCtx {
-    uint8_t* __restrict__ base;
-    uint64_t S, L;
-    uint32_t p;
-    const uint8_t* __restrict__ pay;
-    uint64_t P;
+    const EncodeRows& r;
     u32x2_a4 buf[kPrefetch];
 
     template <int J>
     __device__ __forceinline__ void fetch() {
         if constexpr (J < D) {
             if constexpr (MODE == 2) {
-                const uint64_t o = (uint64_t)J * L + 4 * (uint64_t)p - 4;  // payload byte of value byte J*L + 4p
-                buf[J % kPrefetch] = *reinterpret_cast<const u32x2_a4*>(pay + (o & ~3ull));
+                // payload byte of value byte J*L + 4p, rounded down to 4 (the
+                // byte shift J*L mod 4 is uniform)
+                buf[J % kPrefetch] = payload_window<J>(r, r.p0);
             } else if constexpr (MODE == 0) {
-                buf[J % kPrefetch].x = reinterpret_cast<const uint32_t*>(base + (uint64_t)J * S)[p];
+                buf[J % kPrefetch].x =
+                    __builtin_amdgcn_raw_buffer_load_b32(r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), 0);
             }
         }
     }
 
     template <int J>
     __device__ __forceinline__ uint32_t word() {
-        uint32_t* row = reinterpret_cast<uint32_t*>(base + (uint64_t)J * S);
         uint32_t w;
-        if constexpr (MODE == 2) {
-            const uint64_t o = (uint64_t)J * L + 4 * (uint64_t)p - 4;
-            w = __builtin_amdgcn_alignbyte(buf[J % kPrefetch].y, buf[J % kPrefetch].x, (uint32_t)(o & 3));
-            row[p] = w;
+        if constexpr (MODE == 2 || MODE == 3) {
+            const uint32_t sh = (uint32_t)(((uint64_t)J * r.L) & 3);
+            const u32x2_a4 b = MODE == 2 ? buf[J % kPrefetch] : r.pre[J];
+            w = __builtin_amdgcn_alignbyte(b.y, b.x, sh);
         } else if constexpr (MODE == 1) {
-            w = value_word(pay, P, (uint64_t)J * L + 4 * (uint64_t)p);
-            row[p] = w;
+            w = value_word(r.pay, r.P, (uint64_t)J * r.L + 4 * ((uint64_t)r.p0 + r.t));
         } else {
             w = buf[J % kPrefetch].x;
         }
+        if constexpr (MODE != 0)
+            __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), 0);
         return w;
     }
 
@@ -128,17 +160,19 @@ struct EncodeCtx {
     }
 };
 
+// Column p0 + t of every row: data words (MODE 1/2: from the payload, stored
+// to the data rows) and the Q parity words.
 template <int D, int Q, int MODE>
-__device__ __forceinline__ void encode_word(uint8_t* __restrict__ base, uint64_t S, uint64_t L, uint32_t p,
-                                            const uint8_t* __restrict__ pay, uint64_t P) {
-    EncodeCtx<D, Q, MODE> cx{base, S, L, p, pay, P, {}};
+__device__ __forceinline__ void encode_word(const EncodeRows& r) {
+    EncodeCtx<D, Q, MODE> cx{r, {}};
     uint32_t acc[Q];
 #pragma unroll
     for (int k = 0; k < Q; ++k) acc[k] = 0u;
     cx.prologue(std::make_integer_sequence<int, kPrefetch - 1>{});
     cx.columns(acc, std::make_integer_sequence<int, D>{});
 #pragma unroll
-    for (int k = 0; k < Q; ++k) reinterpret_cast<uint32_t*>(base + (uint64_t)(D + k) * S)[p] = acc[k];
+    for (int k = 0; k < Q; ++k)
+        __builtin_amdgcn_raw_buffer_store_b32(acc[k], r.sh, r.vsh, (uint32_t)((uint64_t)(D + k) * r.S + 4 * r.p0), 0);
 }
 
 // One thread = 4 byte positions of one instance, all N shards; one 256-thread
@@ -166,22 +200,23 @@ __global__ __launch_bounds__(256, 4) void rs_encode_const(uint8_t* __restrict__ 
     if (inst >= n) return;
     uint8_t* base = shards + inst * (uint64_t)(D + Q) * S;
     const uint32_t blk = lb % blocks_per_inst;
-    const uint32_t p = blk * 256 + threadIdx.x;
+    const uint32_t p0 = blk * 256, p = p0 + threadIdx.x;
+    const uint8_t* pay = FROM_PAYLOAD ? payloads + inst * pstride : base;
+    const uint64_t P = FROM_PAYLOAD ? plen[inst] : 0;
+    EncodeRows r{raw_rsrc(base), raw_rsrc(pay), 4 * threadIdx.x, 4 * threadIdx.x, S, L, p0, threadIdx.x, base, pay, P};
     if constexpr (FROM_PAYLOAD) {
-        const uint8_t* pay = payloads + inst * pstride;
-        const uint64_t P = plen[inst];
         if (!payload_fits(P, pstride, D, L)) return;  // device-mode argument check (flagged by rbc_check_plen)
         const uint64_t end = 4 * (uint64_t)(blk * 256 + 256);  // value-byte end of this block in a row
         // interior: past the length prefix, inside the row, and the last row's
         // dwordx2 window [.., (D-1)L + end + 4) inside the payload (+4 prefix)
         const bool interior = blk > 0 && end <= L && (uint64_t)(D - 1) * L + end + 4 <= P + 4;
         if (interior) {
-            encode_word<D, Q, 2>(base, S, L, p, pay, P);
+            encode_word<D, Q, 2>(r);
         } else if (4 * (uint64_t)p < L) {
-            encode_word<D, Q, 1>(base, S, L, p, pay, P);
+            encode_word<D, Q, 1>(r);
         }
     } else {
-        if (4 * (uint64_t)p < L) encode_word<D, Q, 0>(base, S, L, p, nullptr, 0);
+        if (4 * (uint64_t)p < L) encode_word<D, Q, 0>(r);
     }
 }
 
@@ -477,6 +512,212 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
     }
 }
 
+// ============================================================== fused send_shards
+// rbc_encode_merkle<D,Q>: hbbft send_shards (a2 prefix/pad/chunk, a3
+// Coding::encode, a4 MerkleTree::from_vec) in ONE launch.  A workgroup owns
+// IPB instances, LPI = next_pow2(N) lanes each.  The row sweep alternates two
+// phases over the same lanes:
+//   encode pass  lane = column: LPI 4-byte columns of every row of its
+//                instance (the constant-matrix split-nibble coder,
+//                encode_word), stored to the shard rows (written once);
+//   absorb       lane = row: every 136-byte Keccak block that the passes so
+//                far have completed is read back by its row's lane and
+//                absorbed (Keccak-f, keccak_asm.h).
+// The read-back is of bytes this workgroup stored moments earlier, so it is
+// served by L2 (sc1 loads: the vector L1 may hold a stale copy of a line the
+// previous block's loads touched before the pass wrote it), not by a second
+// sweep of 25 GB through HBM as in rs_encode_const -> merkle_build.
+// Addressing: raw buffer resources over the workgroup's shard and payload
+// blocks, row offsets in SGPRs, the lane's offsets in VGPRs.
+// Then the leaf digests and hbbft's tree (odd node promoted) in LDS.
+template <int D, int Q>
+struct FusedShape {
+    static constexpr uint32_t N = D + Q;
+    static constexpr uint32_t LPI = N <= 1 ? 1 : (N <= 2 ? 2 : (N <= 4 ? 4 : (N <= 8 ? 8 : (N <= 16 ? 16 : (N <= 32 ? 32 : (N <= 64 ? 64 : (N <= 128 ? 128 : 256)))))));
+    static constexpr uint32_t BLK = LPI < 64 ? 64 : LPI;
+    static constexpr uint32_t IPB = BLK / LPI;
+    static constexpr uint32_t NODES = merkle_nodes(N);
+    static constexpr int WPE = N <= 64 ? 3 : 2;  // waves per SIMD the register budget is sized for
+};
+
+template <int D, int Q>
+__global__ __launch_bounds__((FusedShape<D, Q>::BLK)) __attribute__((amdgpu_waves_per_eu(FusedShape<D, Q>::WPE)))
+void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint64_t n,
+                       const uint8_t* __restrict__ payloads, uint64_t pstride, const uint64_t* __restrict__ plen,
+                       uint8_t* __restrict__ levels) {
+    using F = FusedShape<D, Q>;
+    constexpr uint32_t N = F::N, LPI = F::LPI, NODES = F::NODES;
+    // LDS: each lane's Keccak state is parked here during an encode pass (its
+    // 50 VGPRs go to the coder), then the leaf digests and tree levels
+    constexpr uint32_t kStash = F::BLK * 25, kTree = F::IPB * NODES * 4;
+    __shared__ uint64_t lds[kStash > kTree ? kStash : kTree];
+    uint32_t* tree_all = reinterpret_cast<uint32_t*>(lds);
+    // IPB == 1: one instance per workgroup, so every instance quantity is
+    // wave-uniform (SGPR bases for the encoder's row addresses)
+    const uint32_t sub = F::IPB == 1 ? 0u : threadIdx.x / LPI, t = F::IPB == 1 ? threadIdx.x : threadIdx.x % LPI;
+    const uint64_t inst = (uint64_t)blockIdx.x * F::IPB + sub;
+    const uint8_t* pay = payloads + inst * pstride;
+    const uint64_t P = inst < n ? plen[inst] : 0;
+    // device-mode argument check (flagged by rbc_check_plen): such an instance
+    // is left unwritten (no shards, no levels)
+    const bool live = inst < n && payload_fits(P, pstride, D, L);
+    uint8_t* base = shards + inst * (uint64_t)N * S;
+    uint32_t* tree = tree_all + sub * NODES * 8;
+    const uint64_t cols = (L + 3) / 4;
+    const uint32_t passes = (uint32_t)((cols + LPI - 1) / LPI);
+    const bool row_lane = live && t < N;
+    // buffer resources over the workgroup's first instance (uniform); a lane's
+    // instance and column / row are VGPR offsets (host: IPB * N * S and
+    // IPB * pstride < 2^31)
+    const uint64_t inst0 = (uint64_t)blockIdx.x * F::IPB;
+    EncodeRows r{raw_rsrc(shards + inst0 * N * S), raw_rsrc(payloads + inst0 * pstride),
+                 (uint32_t)(sub * N * S) + 4 * t, (uint32_t)(sub * pstride) + 4 * t, S, L, 0, t, base, pay, P};
+    const uint32_t vrow = (uint32_t)((sub * N + t) * S);  // absorb: this lane's row
+    u64p a[25];
+    keccak_zero(a);
+    uint32_t done = 0;  // 136-byte blocks absorbed (the same count for every row)
+    // interior pass (MODE 2/3 legal): past the length prefix, inside the row,
+    // the last row's window inside the payload
+    auto interior = [&](uint32_t ps) {
+        const uint64_t end = 4ull * ((uint64_t)ps * LPI + LPI);  // value-byte end of the pass in a row
+        return ps > 0 && end <= L && (uint64_t)(D - 1) * L + end + 4 <= P + 4;
+    };
+    u32x2_a4 pre[D];  // the next interior pass's payload windows, loaded during this pass's Keccak work
+    r.pre = pre;
+    bool have_pre = false;
+    for (uint32_t ps = 0; ps < passes; ++ps) {
+        const uint32_t p0 = ps * LPI, p = p0 + t;  // this lane's column in the encode pass
+        r.p0 = p0;
+        if (done > 0) {  // park the sponge state (nothing absorbed yet: it is zero)
+#pragma unroll
+            for (int i = 0; i < 25; ++i) lds[i * F::BLK + threadIdx.x] = ((uint64_t)a[i].hi << 32) | a[i].lo;
+        }
+        if (live) {
+            if (have_pre) {
+                encode_word<D, Q, 3>(r);
+            } else if (interior(ps)) {
+                encode_word<D, Q, 2>(r);
+            } else if (4 * (uint64_t)p < L) {
+                encode_word<D, Q, 1>(r);
+            }
+        }
+        // the pass's stores are complete in L2 before any lane reads them back
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (F::BLK > 64) __syncthreads();
+        if (done > 0) {
+#pragma unroll
+            for (int i = 0; i < 25; ++i) {
+                const uint64_t v = lds[i * F::BLK + threadIdx.x];
+                a[i] = {(uint32_t)v, (uint32_t)(v >> 32)};
+            }
+        } else {
+            keccak_zero(a);
+        }
+        const uint64_t written = 4ull * LPI * (ps + 1);
+        const uint64_t avail = written < L ? written : L;
+        const bool next_pre = live && ps + 1 < passes && interior(ps + 1);
+        have_pre = false;
+        auto prefetch = [&]() {
+            if (next_pre && !have_pre) {
+                [&]<int... J>(std::integer_sequence<int, J...>) {
+                    ((pre[J] = payload_window<J>(r, p0 + LPI)), ...);
+                }(std::make_integer_sequence<int, D>{});
+            }
+            have_pre = next_pre;
+        };
+        while ((uint64_t)(done + 1) * 136 <= avail) {
+            if (row_lane) {
+                uint64_t w[17];
+#pragma unroll
+                for (int i = 0; i < 17; ++i) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.sh, vrow + 8 * i, 136 * done, kBufSc1);
+                    w[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                }
+#pragma unroll
+                for (int i = 0; i < 17; ++i) {
+                    a[i].lo ^= (uint32_t)w[i];
+                    a[i].hi ^= (uint32_t)(w[i] >> 32);
+                }
+            }
+            // next pass's payload loads: behind this block's loads (vmcnt is
+            // in order), ahead of a whole permutation
+            prefetch();
+            if (row_lane) perm<1>(a);
+            ++done;
+        }
+        prefetch();
+    }
+    uint32_t d[8];
+    if (row_lane) {
+        // final (possibly empty) block: bytes [136 done, L) + FIPS-202 padding.
+        // Reads stay below round_up(L, 8) <= S.
+        const uint32_t rem = (uint32_t)(L - (uint64_t)done * 136);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            uint64_t w = 0;
+            if ((uint32_t)(8 * i) < rem) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.sh, vrow + 8 * i, 136 * done, kBufSc1);
+                w = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                const uint32_t left = rem - 8 * i;
+                if (left < 8) w &= ~0ull >> (64 - 8 * left);
+            }
+            a[i].lo ^= (uint32_t)w;
+            a[i].hi ^= (uint32_t)(w >> 32);
+        }
+        const uint32_t wi = rem >> 3, sh = (rem & 7) * 8;
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            if ((uint32_t)i == wi) {
+                if (sh < 32) a[i].lo ^= 0x06u << sh;
+                else a[i].hi ^= 0x06u << (sh - 32);
+            }
+        }
+        a[16].hi ^= 0x80000000u;
+        perm<1>(a);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            d[2 * i] = a[i].lo;
+            d[2 * i + 1] = a[i].hi;
+        }
+    }
+    uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)NODES * 32);
+    __syncthreads();  // the tree reuses the state stash
+    if (row_lane) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tree[t * 8 + i] = d[i];
+        gout[2 * t] = make_uint4(d[0], d[1], d[2], d[3]);
+        gout[2 * t + 1] = make_uint4(d[4], d[5], d[6], d[7]);
+    }
+    __syncthreads();
+    uint32_t lbase = 0, cnt = N;
+    while (cnt > 1) {
+        const uint32_t nn = (cnt + 1) / 2;
+        if (live && t < nn) {
+            uint32_t h[8];
+            if (2 * t + 1 < cnt) {
+                uint32_t l[8], r[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    l[i] = tree[(lbase + 2 * t) * 8 + i];
+                    r[i] = tree[(lbase + 2 * t + 1) * 8 + i];
+                }
+                sha3_pair<1>(l, r, h);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) h[i] = tree[(lbase + 2 * t) * 8 + i];
+            }
+            const uint32_t at = lbase + cnt + t;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tree[at * 8 + i] = h[i];
+            gout[2 * at] = make_uint4(h[0], h[1], h[2], h[3]);
+            gout[2 * at + 1] = make_uint4(h[4], h[5], h[6], h[7]);
+        }
+        __syncthreads();
+        lbase += cnt;
+        cnt = nn;
+    }
+}
+
 // Proof::validate(N) — one work-item per proof.
 __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len, const uint8_t* __restrict__ values,
                                                        uint64_t vstride, const uint32_t* __restrict__ index,
@@ -637,6 +878,19 @@ bool has_const_encoder(uint32_t D, uint32_t Q) {
     return (D == 2 && Q == 2) || (D == 6 && Q == 10) || (D == 22 && Q == 42) || (D == 44 && Q == 84);
 }
 
+// The constant encoders address rows through raw buffer resources of 2^31
+// bytes (raw_rsrc): a workgroup's shard block and payload block must fit.
+bool const_encoder_fits(uint32_t D, uint32_t Q, uint64_t S, uint64_t pstride, bool fused) {
+    uint64_t ipb = 1;
+    if (fused) {
+        uint32_t lpi = 1;
+        while (lpi < D + Q) lpi <<= 1;
+        ipb = lpi < 64 ? 64 / lpi : 1;
+    }
+    const uint64_t lim = 1ull << 31;
+    return has_const_encoder(D, Q) && ipb * (D + Q) * S < lim && ipb * (pstride + 16) < lim;
+}
+
 hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen,
                                   hipStream_t st) {
@@ -644,6 +898,26 @@ hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint6
     if (D == 6 && Q == 10) return launch_encode_const<6, 10>(shards, S, L, n, payloads, pstride, plen, st);
     if (D == 22 && Q == 42) return launch_encode_const<22, 42>(shards, S, L, n, payloads, pstride, plen, st);
     if (D == 44 && Q == 84) return launch_encode_const<44, 84>(shards, S, L, n, payloads, pstride, plen, st);
+    return hipErrorInvalidValue;
+}
+
+template <int D, int Q>
+static hipError_t launch_fused(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n, const uint8_t* payloads,
+                               uint64_t pstride, const uint64_t* plen, uint8_t* levels, hipStream_t st) {
+    using F = FusedShape<D, Q>;
+    const uint64_t blocks = (n + F::IPB - 1) / F::IPB;
+    rbc_encode_merkle<D, Q><<<dim3((uint32_t)blocks), dim3(F::BLK), 0, st>>>(shards, S, L, n, payloads, pstride,
+                                                                             plen, levels);
+    return hipGetLastError();
+}
+
+hipError_t launch_rbc_encode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                    const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, uint8_t* levels,
+                                    hipStream_t st) {
+    if (D == 2 && Q == 2) return launch_fused<2, 2>(shards, S, L, n, payloads, pstride, plen, levels, st);
+    if (D == 6 && Q == 10) return launch_fused<6, 10>(shards, S, L, n, payloads, pstride, plen, levels, st);
+    if (D == 22 && Q == 42) return launch_fused<22, 42>(shards, S, L, n, payloads, pstride, plen, levels, st);
+    if (D == 44 && Q == 84) return launch_fused<44, 84>(shards, S, L, n, payloads, pstride, plen, levels, st);
     return hipErrorInvalidValue;
 }
 

@@ -346,3 +346,44 @@ def test_device_batch_mixed_payload_lengths():
         rs, rl = corc.rbc_encode_merkle(N, pays[k].copy())
         assert np.array_equal(sh[k, :, :L], rs), k
         assert np.array_equal(lv[k], rl), k
+
+
+@pytest.mark.parametrize("N,P,n", [(64, 1 << 20, 5), (16, 65536, 21), (128, 1 << 20, 3), (4, 230, 70), (64, 5000, 9)])
+def test_fused_schedule_matches_two_launch_schedule(N, P, n):
+    """hbg_test_set_rbc_fused: the single-launch rbc_encode_merkle kernel
+    (encode pass + SHA3 leaves + tree) writes the same shards
+    and levels as rs_encode_const -> merkle_build, and both match the oracle
+    on sampled instances (mixed payload lengths that share L included)."""
+    torch = _torch()
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    L = _lib.shard_len(N, P)
+    D, _ = bc.shard_counts(N)
+    lens = [P if k % 3 else max(1, D * L - 4 - (k % 4)) for k in range(n)]
+    assert all(_lib.shard_len(N, p) == L for p in lens)
+    S = (L + 15) // 16 * 16
+    PS = (max(lens) + 15) // 16 * 16
+    dev = torch.device("cuda:0")
+    pays = [np.frombuffer(synth.payload(2100 + k, p), np.uint8) for k, p in enumerate(lens)]
+    host = np.zeros((n, PS), np.uint8)
+    for k, p in enumerate(pays):
+        host[k, :len(p)] = p
+    pay = torch.from_numpy(host).to(dev)
+    plen = torch.tensor(lens, dtype=torch.int64, device=dev)
+    out = []
+    ctx = _lib.Context(0)
+    try:
+        for fused in (0, 1):
+            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, fused))
+            shards = torch.full((n, N, S), 0xA5, dtype=torch.uint8, device=dev)
+            levels = torch.full((n, _lib.merkle_nodes(N), 32), 0x5A, dtype=torch.uint8, device=dev)
+            bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels, ctx=ctx, device=True)
+            torch.cuda.synchronize()
+            out.append((shards[:, :, :L].cpu().numpy(), levels.cpu().numpy()))
+    finally:
+        ctx.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    for k in (0, n // 2, n - 1):
+        rs, rl = corc.rbc_encode_merkle(N, pays[k].copy())
+        assert np.array_equal(out[1][0][k], rs), k
+        assert np.array_equal(out[1][1][k], rl), k

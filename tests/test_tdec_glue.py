@@ -198,3 +198,59 @@ def test_device_generated_epoch_and_driver():
     assert st.cpu().tolist() == [0] * 96
     assert np.array_equal(oc.cpu().numpy(), tw.expected_outcomes(ep.bad, ep.t))
     assert torch.equal(pt, ep.msgs)
+
+
+@pytest.mark.gpu
+def test_configs3_size_threshold_decrypt_100k():
+    """BASELINE.json configs[3] at full size: 100,000 distinct ciphertexts x 64
+    shares (N = 64, t = 21, 1 % bad shares of the three kinds) through
+    hbg_tdec_verify_shares and hbg_tdec_threshold_decrypt (device mode).  The
+    round-2 grid-stride kernels faulted at >= 65,536 ciphertexts; this is the
+    size that has to hold.  Checks: every share bit against construction,
+    every outcome byte and plaintext against construction, and a sample of
+    ciphertexts (every one holding a bad share among them) bit for bit against
+    the C oracle's per-share verify_decryption_share and PublicKeySet::decrypt."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import _lib, tdec_workload as tw
+    from oracle import corb
+    th = _th()
+    dev = torch.device("cuda:0")
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    n_ct, N, L = 100_000, 64, 256
+    ep = tw.make_epoch(ctx, dev, n_ct=n_ct, n_nodes=N, msg_len=L, bad_rate=0.01, seed=11)
+    n = n_ct * N
+    sct = torch.arange(n_ct, dtype=torch.int32, device=dev).repeat_interleave(N)
+    spk = torch.arange(N, dtype=torch.int32, device=dev).repeat(n_ct)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    _lib.check(_lib.lib().hbg_tdec_verify_shares(ctx.h, n_ct, ep.U.data_ptr(), ep.V.data_ptr(), ep.V_off.data_ptr(),
+                                                 ep.W.data_ptr(), N, ep.pk48.data_ptr(), n, ep.share48.data_ptr(),
+                                                 sct.data_ptr(), spk.data_ptr(), ok.data_ptr(), _lib.HBG_DEVICE),
+               "verify_decryption_share")
+    okh = ok.cpu().numpy().reshape(n_ct, N).astype(bool)
+    assert np.array_equal(okh, ~ep.bad)
+    pt = torch.zeros(n_ct * L, dtype=torch.uint8, device=dev)
+    st = torch.zeros(n_ct, dtype=torch.int32, device=dev)
+    oc = torch.zeros((n_ct, N), dtype=torch.uint8, device=dev)
+    th.threshold_decrypt_arrays(ep.t, N, ep.U, ep.V, ep.V_off, ep.W, ep.pk48, ep.share48, None, pt, st, oc,
+                                ctx=ctx, device=True)
+    assert st.cpu().tolist() == [0] * n_ct
+    assert np.array_equal(oc.cpu().numpy(), tw.expected_outcomes(ep.bad, ep.t))
+    assert torch.equal(pt, ep.msgs)
+    # sampled oracle comparison: ciphertexts with a bad share, spread over the batch
+    bad_rows = np.nonzero(ep.bad.any(axis=1))[0]
+    sample = sorted(set(bad_rows[:: max(1, len(bad_rows) // 6)][:6].tolist() + [0, n_ct // 2, n_ct - 1]))
+    U, V, W = ep.U.cpu().numpy(), ep.V.cpu().numpy(), ep.W.cpu().numpy()
+    pk = [ep.pk48[i].cpu().numpy().tobytes() for i in range(N)]
+    sh = ep.share48.cpu().numpy()
+    cts = [(U[k].tobytes(), V[L * k:L * (k + 1)].tobytes(), W[k].tobytes()) for k in sample]
+    items = [(sh[k, i].tobytes(), j, i) for j, k in enumerate(sample) for i in range(N)]
+    ref = corb.verify_shares(cts, pk, items, threads=8).reshape(len(sample), N)
+    assert np.array_equal(ref.astype(bool), okh[sample])
+    sel = [[(i, sh[k, i].tobytes()) for i in range(N) if okh[k, i]][: ep.t + 1] for k in sample]
+    pts, rst = corb.decrypt_batch(ep.t, cts, sel, threads=8)
+    ph = pt.cpu().numpy()
+    assert rst.tolist() == [0] * len(sample)
+    assert pts == [ph[L * k:L * (k + 1)].tobytes() for k in sample]

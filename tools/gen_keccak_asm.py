@@ -45,12 +45,15 @@ class Alloc:
             i += 1
 
 
-def layout():
-    """Returns (round body lines, A[x][y][h] register map, registers used)."""
+def layout(hshift: int = 0):
+    """Returns (round body lines, A[x][y][h] register map, registers used).
+    hshift: bank offset of a lane's hi word relative to its lo word (2 puts
+    the two halves in different banks, so the rho v_alignbit reading both
+    halves has no source bank conflict)."""
     al = Alloc(0)
     # A[x][y][h]: bank (x + y) mod 4 — column triples y=0,1,2 distinct, y=3,4
     # distinct, partial-C bank free; spreads the state evenly over the banks
-    A = [[[al.take((x + y) % 4) for h in range(2)] for y in range(5)] for x in range(5)]
+    A = [[[al.take((x + y + hshift * h) % 4) for h in range(2)] for y in range(5)] for x in range(5)]
     bbank = [0, 1, 2, 3, 1]  # per row, rotated by y below
     B = [[[None, None] for y in range(5)] for x in range(5)]
     for x in range(5):
@@ -59,7 +62,7 @@ def layout():
                 if x == 0 and y == 0:
                     B[x][y][h] = A[0][0][h]  # alias (rotation 0)
                 else:
-                    B[x][y][h] = al.take((bbank[x] + y) % 4)
+                    B[x][y][h] = al.take((bbank[x] + y + hshift * h) % 4)
     # theta temporaries live only before B is written: they reuse B registers.
     pool = [B[x][y][h] for x in range(5) for y in range(5) for h in range(2) if not (x == 0 and y == 0)]
 
@@ -71,8 +74,10 @@ def layout():
         raise RuntimeError("pool exhausted")
 
     taken = set()
-    Cp = [[from_pool({(x + 1) % 4, (x + 2) % 4}, taken) for h in range(2)] for x in range(5)]  # partial C
-    C = [[from_pool({0, 1, 2, 3}, taken) for h in range(2)] for x in range(5)]
+    Cp = [[from_pool({(x + 1 + hshift * h) % 4, (x + 2 + hshift * h) % 4}, taken) for h in range(2)]
+          for x in range(5)]  # partial C
+    C = [[from_pool({0, 1, 2, 3} if not hshift else {(2 * h) % 4, (2 * h + 1) % 4}, taken) for h in range(2)]
+         for x in range(5)]
     T = [[from_pool({0, 1, 2, 3}, taken), from_pool({0, 1, 2, 3}, taken)] for x in range(5)]
     D = Cp  # D is written after Cp is dead (no bank constraint on D)
     regs_used = sorted(al.used)

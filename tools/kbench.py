@@ -68,6 +68,12 @@ def main():
         if "encode" in whats:
             res["encode_merkle_ms"] = t(lambda: bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels, ctx=ctx,
                                                                           device=True, asynchronous=True))
+        if "fused" in whats:  # the single-launch schedule (hbg_test_set_rbc_fused)
+            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, 1))
+            res["encode_merkle_fused_ms"] = t(lambda: bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels,
+                                                                                ctx=ctx, device=True,
+                                                                                asynchronous=True))
+            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, 0))
         if "rs" in whats:
             def rs():
                 _lib.check(_lib.lib().hbg_rs_encode(ctx.h, D, Q, L, shards.data_ptr(), S, B,
