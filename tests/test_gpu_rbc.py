@@ -359,7 +359,7 @@ def test_fused_schedule_matches_two_launch_schedule(N, P, n):
     from hydrabadger_amd import _lib
     L = _lib.shard_len(N, P)
     D, _ = bc.shard_counts(N)
-    lens = [P if k % 3 else max(1, D * L - 4 - (k % 4)) for k in range(n)]
+    lens = [P if k % 3 else D * L - 4 - (k % min(4, D)) for k in range(n)]
     assert all(_lib.shard_len(N, p) == L for p in lens)
     S = (L + 15) // 16 * 16
     PS = (max(lens) + 15) // 16 * 16
