@@ -26,7 +26,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 40;
+constexpr int kNumSlots = 44;
 
 struct Buf {
     void* p = nullptr;
@@ -42,9 +42,10 @@ struct hbg_ctx {
     Buf slot[kNumSlots];
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> matrices;  // device (D+Q) x D coding matrices
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> enc_plans; // device shared encode plans
-    // share verification schedule (hbg_test_set_tdec_batched / HBG_TDEC_BATCHED): 0 per share, 1 batched
-    // (pk fixed-base tables when each key verifies >= kPkTableMinUses shares), 2 batched + tables always
-    // (and, for signature shares, no speculative 16-group round)
+    // share verification schedule (hbg_test_set_tdec_batched): 0 per share; 1 (default) batched from
+    // kBatchMinShares shares up, per share below (latency: a batched call is several dependent check
+    // rounds); 2 batched + pk tables always (and, for signature shares, no speculative 16-group round);
+    // 3 batched at every size.  pk fixed-base tables when each key verifies >= kPkTableMinUses shares.
     int tdec_batched = 1;
     // hbg_rbc_encode_merkle schedule (hbg_test_set_rbc_fused): 0 rs_encode_const + merkle_build, 1 fused
     int rbc_fused = 0;
@@ -586,7 +587,10 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     t.coefH = (uint32_t*)ph;
     t.coefW = (uint32_t*)pwc;
     HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
-    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW, c->stream));
+    void* pdg;
+    HBG_CHECK(scratch(c, 40, 32ull * n_ct, &pdg));
+    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW,
+                                        (uint8_t*)pdg, c->stream));
     return HBG_OK;
 }
 
@@ -608,6 +612,16 @@ int prepare_pks(hbg_ctx* c, uint32_t n_pk, const uint8_t* dpk, void** paff, void
 // A pk table costs ~2k G1 scalar multiplications to build and saves ~60 G1
 // doublings per share verified under that key.
 constexpr uint64_t kPkTableMinUses = 2048;
+
+// Below this many shares a batched verification (leaves + up to four dependent
+// check rounds, each at most a few waves deep) takes longer than checking
+// every share at once: one round of independent pairing checks over
+// 1,024 SIMDs x 2 waves x 64 lanes (measured crossover).
+constexpr uint64_t kBatchMinShares = 3ull * 1024 * 2 * 64;
+bool use_batched(const hbg_ctx* c, uint64_t n) {
+    if (c->tdec_batched == 0 || n < 2 || n >= (1ull << 31)) return false;
+    return c->tdec_batched >= 2 || n >= kBatchMinShares;
+}
 
 int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uint8_t* dU48, uint32_t n,
                           uint32_t n_pk, const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp,
@@ -768,7 +782,7 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     void *paff, *pst;
     HBG_CHECK(prepare_pks(c, n_pk, dpk, &paff, &pst));
     HBG_DBG_STEP(c, "pk_prepare");
-    if (c->tdec_batched && n >= 2 && n < (1ull << 31)) {
+    if (use_batched(c, n)) {
         HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, n_pk, dsh, dsc, dsp, (const uint32_t*)paff,
                                         (const int32_t*)pst, dok));
     } else {
@@ -841,9 +855,11 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
         dout = (uint8_t*)o;
         dst = (int32_t*)s;
     }
-    void* scr;
+    void *scr, *sds;
     HBG_CHECK(scratch(c, 6, 4ull * 32 * m * n_ct, &scr));
-    HBG_TRY(bls::launch_tdec_combine(n_ct, t, dsh, dix, dV, dVoff, dout, dst, (uint32_t*)scr, c->stream));
+    HBG_CHECK(scratch(c, 41, 32ull * n_ct, &sds));
+    HBG_TRY(bls::launch_tdec_combine(n_ct, t, dsh, dix, dV, dVoff, dout, dst, (uint32_t*)scr, (uint8_t*)sds,
+                                     c->stream));
     if (!(flags & HBG_DEVICE)) {
         if (vlen) HBG_TRY(hipMemcpyAsync(out, dout, vlen, hipMemcpyDeviceToHost, c->stream));
         HBG_TRY(hipMemcpyAsync(status, dst, 4ull * n_ct, hipMemcpyDeviceToHost, c->stream));
@@ -920,7 +936,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_TRY(bls::launch_tdec_pair_index(n, n_nodes, sct, spk, c->stream));
     void *paff, *pst;
     HBG_CHECK(prepare_pks(c, n_nodes, (const uint8_t*)dpk, &paff, &pst));
-    if (c->tdec_batched && n >= 2) {
+    if (use_batched(c, n)) {
         HBG_CHECK(verify_shares_batched(c, n_ct, tab, tab.U48, (uint32_t)n, n_nodes, (const uint8_t*)dsh, sct, spk,
                                         (const uint32_t*)paff, (const int32_t*)pst, (uint8_t*)okb));
     } else {
@@ -937,10 +953,11 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
                                     (const uint32_t*)darr, (const uint8_t*)dsh, sidx, s48, (uint8_t*)doc, sst,
                                     c->stream));
     // PublicKeySet::decrypt (interpolate + xor_with_hash) of the selections
-    void* scr;
+    void *scr, *sds;
     HBG_CHECK(scratch(c, 39, 4ull * 32 * m * n_ct, &scr));
+    HBG_CHECK(scratch(c, 41, 32ull * n_ct, &sds));
     HBG_TRY(bls::launch_tdec_combine(n_ct, t, s48, sidx, dV, dVoff, (uint8_t*)dpt, (int32_t*)dst, (uint32_t*)scr,
-                                     c->stream));
+                                     (uint8_t*)sds, c->stream));
     HBG_TRY(bls::launch_tdec_status_merge(n_ct, sst, (int32_t*)dst, c->stream));
     return drain(c, flags, {{plaintext, {dpt, vlen}}, {status, {dst, 4ull * n_ct}}, {outcome, {doc, n}}});
 }
@@ -1014,9 +1031,14 @@ int hbg_tdec_encrypt(hbg_ctx* c, const uint8_t* pk48, uint64_t n, const uint8_t*
     HBG_CHECK(stage_out(c, flags, 9, W96, 96ull * n, &dW));
     HBG_CHECK(prepare_pks(c, 1, (const uint8_t*)dpk, &paff, &pst));
     // an undecodable pk: HBG_E_INVALID_POINT from the kernel (returned at the next synchronisation point)
+    void *sds, *sdg, *sst;
+    HBG_CHECK(scratch(c, 41, 32ull * n, &sds));
+    HBG_CHECK(scratch(c, 42, 32ull * n, &sdg));
+    HBG_CHECK(scratch(c, 43, 4ull * n, &sst));
     HBG_TRY(bls::launch_tdec_encrypt(n, (const uint32_t*)paff, (const int32_t*)pst, (const uint8_t*)dr,
                                      (const uint8_t*)dm, (const uint64_t*)doff, (uint8_t*)dU, (uint8_t*)dV,
-                                     (uint8_t*)dW, c->d_err, c->stream));
+                                     (uint8_t*)dW, (uint8_t*)sds, (uint8_t*)sdg, (int32_t*)sst, c->d_err,
+                                     c->stream));
     return drain(c, flags, {{U48, {dU, 48ull * n}}, {V, {dV, mlen}}, {W96, {dW, 96ull * n}}});
 }
 
@@ -1109,7 +1131,7 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
     const uint8_t* sh = (const uint8_t*)dsh;
     uint8_t* o = (uint8_t*)dok;
     const uint32_t* ch = (const uint32_t*)coefH;
-    if (!(c->tdec_batched && n >= 2 && n < (1ull << 31))) {
+    if (!use_batched(c, n)) {
         HBG_TRY(bls::launch_sig_verify_shares(n, nullptr, nullptr, sh, sd, sp, pa, ps, ch, (uint32_t*)lines, o,
                                               c->stream));
         return drain(c, flags, {{ok, {dok, n}}});
@@ -1183,7 +1205,7 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (on < 0 || on > 2) return HBG_E_ARG;
+    if (on < 0 || on > 3) return HBG_E_ARG;
     c->tdec_batched = on;
     return HBG_OK;
 }

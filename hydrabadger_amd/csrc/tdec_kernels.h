@@ -21,9 +21,14 @@ constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G
 // their per-lane scratch (G2Prepared lines) is sized for kResidentBlocks * 64.
 constexpr uint32_t kResidentBlocks = 2048;
 
+// vdig: [n][32] scratch for SHA3(V) of the items with |V| > 64 (tdec_v_digest)
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
-                                  uint32_t* coefW, hipStream_t st);
+                                  uint32_t* coefW, uint8_t* vdig, hipStream_t st);
+// xor_with_hash's keystream: out = in ^ keystream(seeds[k]) per item (status[k] != 0: skipped; nullable)
+hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uint8_t* in, const uint64_t* off,
+                                     uint8_t* out, const int32_t* status, hipStream_t st);
+hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_off, uint8_t* dig, hipStream_t st);
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st);
 // cap: items the grid is sized for; n_dev (nullable): the device word holding
@@ -63,9 +68,10 @@ hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const i
 hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
                              const uint32_t* msg_pk, const uint8_t* msg, const uint64_t* off, const uint8_t* sig96,
                              uint32_t* lines, uint8_t* ok, int32_t* err, hipStream_t st);
+// seeds / vdig: [n][32] scratch; est: [n] int32 scratch
 hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
                                const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
-                               int32_t* err, hipStream_t st);
+                               uint8_t* seeds, uint8_t* vdig, int32_t* est, int32_t* err, hipStream_t st);
 hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, const uint32_t* u_aff,
                                      const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
                                      const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
@@ -94,9 +100,10 @@ hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8
                               uint8_t* outcome, int32_t* sel_status, hipStream_t st);
 hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st);
 hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32_t* status, hipStream_t st);
+// seeds: [n][32] scratch (xor_with_hash keys, consumed by tdec_keystream_xor)
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
-                               uint32_t* scratch, hipStream_t st);
+                               uint32_t* scratch, uint8_t* seeds, hipStream_t st);
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,
                             uint32_t out_words, uint32_t* lines, hipStream_t st);
 

@@ -19,6 +19,7 @@
 #include "bls.h"
 #include "dev_err.h"
 #include "keccak.h"
+#include "keccak_asm.h"
 #include "tdec_kernels.h"
 
 #include <hipcub/hipcub.hpp>
@@ -154,6 +155,117 @@ struct ChaChaRng {
         return buf[idx++];
     }
 };
+
+// ------------------------------------------------------------------ long messages (a13, a16)
+// xor_with_hash's keystream and hash_g1_g2's SHA3(V) for contributions of any
+// length (in HoneyBadger V is the whole serialised contribution):
+//  * the keystream is seekable by block counter: one 256-thread block per
+//    item, threads over its ChaCha20 blocks; block c covers output bytes
+//    [16c, 16c + 16) (rand's `Standard` u8 is the low byte of each next_u32);
+//  * SHA3(V) reads V a dword at a time (aligned loads + v_alignbyte) into the
+//    bank-allocated Keccak round (keccak_asm.h), one lane per item.
+// Both replace byte-serial loops of one lane in the kernels that call them.
+__global__ __launch_bounds__(256) void tdec_keystream_xor(uint64_t n, const uint8_t* __restrict__ seeds,
+                                                          const uint8_t* __restrict__ in,
+                                                          const uint64_t* __restrict__ off, uint8_t* __restrict__ out,
+                                                          const int32_t* __restrict__ status) {
+    const uint64_t k = blockIdx.x;
+    if (k >= n || (status && status[k] != 0)) return;  // no output for a failed item (its bytes stay untouched)
+    uint32_t key[8];
+    const uint8_t* sd = seeds + 32 * k;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        key[i] = (uint32_t)sd[4 * i] | ((uint32_t)sd[4 * i + 1] << 8) | ((uint32_t)sd[4 * i + 2] << 16) |
+                 ((uint32_t)sd[4 * i + 3] << 24);
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    const uint64_t nb = (len + 15) / 16;
+    for (uint64_t c = threadIdx.x; c < nb; c += blockDim.x) {
+        uint32_t w[16];
+        chacha_block(key, (uint32_t)c, w);
+        const uint64_t b0 = 16 * c;
+#pragma unroll
+        for (int b = 0; b < 16; ++b)
+            if (b0 + b < len) out[o + b0 + b] = in[o + b0 + b] ^ (uint8_t)(w[b] & 0xFFu);
+    }
+}
+
+// SHA3-256 of len bytes at p (any alignment).  An aligned dword holding at
+// least one message byte is always readable.
+__device__ __forceinline__ void sha3_long(const uint8_t* p, uint64_t len, uint8_t* out) {
+    u64p a[25];
+    keccak_zero(a);
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+    uint64_t pos = 0;
+    for (; pos + 136 <= len; pos += 136) {
+        const uint32_t* qb = q + pos / 4;
+        uint32_t w[35];
+#pragma unroll
+        for (int j = 0; j < 34; ++j) w[j] = qb[j];
+        w[34] = sh ? qb[34] : 0u;
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            a[i].lo ^= __builtin_amdgcn_alignbyte(w[2 * i + 1], w[2 * i], sh);
+            a[i].hi ^= __builtin_amdgcn_alignbyte(w[2 * i + 2], w[2 * i + 1], sh);
+        }
+        perm<1>(a);
+    }
+    const uint32_t rem = (uint32_t)(len - pos);  // < 136 bytes + FIPS-202 padding
+    uint32_t w[34];
+#pragma unroll
+    for (int j = 0; j < 34; ++j) w[j] = 0u;
+    for (uint32_t i = 0; i < rem; ++i) {
+        const uint32_t b = p[pos + i];
+#pragma unroll
+        for (int j = 0; j < 34; ++j)
+            if ((i >> 2) == (uint32_t)j) w[j] |= b << (8 * (i & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < 34; ++j) {
+        if ((rem >> 2) == (uint32_t)j) w[j] ^= 0x06u << (8 * (rem & 3));
+    }
+    w[33] ^= 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        a[i].lo ^= w[2 * i];
+        a[i].hi ^= w[2 * i + 1];
+    }
+    perm<1>(a);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            out[8 * i + b] = (uint8_t)(a[i].lo >> (8 * b));
+            out[8 * i + 4 + b] = (uint8_t)(a[i].hi >> (8 * b));
+        }
+    }
+}
+
+// dig[k] = SHA3(V_k) for every item with |V_k| > 64 (hash_g1_g2's message
+// digest); shorter items are hashed inline by the caller.
+__global__ __launch_bounds__(64) void tdec_v_digest(uint64_t n, const uint8_t* __restrict__ V,
+                                                    const uint64_t* __restrict__ off, uint8_t* __restrict__ dig) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    if (len > 64) sha3_long(V + o, len, dig + 32 * k);
+}
+
+// hash_g1_g2's message m = (|V| > 64 ? SHA3(V) : V) || compress(U); returns
+// |m| (dig: tdec_v_digest's output for this item).
+BD uint32_t hash_g1_g2_msg(const uint8_t* V, uint64_t len, const uint8_t* dig, const uint8_t* u48,
+                           uint8_t (&m)[64 + 48]) {
+    uint32_t mlen;
+    if (len > 64) {
+        for (int i = 0; i < 32; ++i) m[i] = dig[i];
+        mlen = 32;
+    } else {
+        for (uint32_t i = 0; i < len; ++i) m[i] = V[i];
+        mlen = (uint32_t)len;
+    }
+    for (int i = 0; i < 48; ++i) m[mlen + i] = u48[i];
+    return mlen + 48;
+}
 
 // ------------------------------------------------------------------ hash_g1_g2
 // ff_derive Rand for Fq: 6 x next_u64 (LE), top limb masked by 3 shave bits,
@@ -405,6 +517,7 @@ BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool us
 TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
                                                       const uint8_t* __restrict__ V,
                                                       const uint64_t* __restrict__ V_off,
+                                                      const uint8_t* __restrict__ vdig,
                                                       const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
                                                       int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH,
                                                       uint32_t* __restrict__ coefW) {
@@ -425,17 +538,9 @@ TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
     // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
     const uint64_t off = V_off[k], len = V_off[k + 1] - off;
     uint8_t m[64 + 48];
-    uint32_t mlen;
-    if (len > 64) {
-        sha3_bytes(V + off, (uint32_t)len, m);
-        mlen = 32;
-    } else {
-        for (uint32_t i = 0; i < len; ++i) m[i] = V[off + i];
-        mlen = (uint32_t)len;
-    }
-    for (int i = 0; i < 48; ++i) m[mlen + i] = U48[48ull * k + i];
+    const uint32_t ml = hash_g1_g2_msg(V + off, len, vdig + 32ull * k, U48 + 48ull * k, m);
     uint8_t seed[32];
-    sha3_bytes(m, mlen + 48, seed);
+    sha3_bytes(m, ml, seed);
     const G2A h = hash_g2_from_seed(seed);
     g2_prepare(h.x, h.y, coefH + (uint64_t)k * 72 * kMillerSteps);
     if (!w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
@@ -990,8 +1095,7 @@ BD Fr fr_canonical(const Fr& a) {
 // shares: [n][t+1][48] compressed (already verified: no subgroup re-check, as
 // in the crate where decrypt consumes parsed shares); idx: [n][t+1] node indices.
 TDEC_KERNEL void tdec_combine(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
-                                                   const uint32_t* __restrict__ idx, const uint8_t* __restrict__ V,
-                                                   const uint64_t* __restrict__ V_off, uint8_t* __restrict__ out,
+                                                   const uint32_t* __restrict__ idx, uint8_t* __restrict__ seeds,
                                                    int32_t* __restrict__ status, uint32_t* __restrict__ scratch) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -1047,12 +1151,7 @@ TDEC_KERNEL void tdec_combine(uint32_t n, uint32_t t, const uint8_t* __restrict_
     const G1A g = g1_to_affine(acc);
     uint8_t cg[48];
     g1_compress(cg, g);
-    uint8_t seed[32];
-    sha3_bytes(cg, 48, seed);
-    ChaChaRng rng;
-    rng.init(seed);
-    const uint64_t off = V_off[k], len = V_off[k + 1] - off;
-    for (uint64_t i = 0; i < len; ++i) out[off + i] = V[off + i] ^ (uint8_t)(rng.next_u32() & 0xFFu);
+    sha3_bytes(cg, 48, seeds + 32ull * k);  // xor_with_hash's key: the keystream runs in tdec_keystream_xor
 }
 
 // GLV split on G1 (Gallant–Lambert–Vanstone): phi(x, y) = (beta x, y) acts as
@@ -1134,9 +1233,7 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
 // one-lane-per-ciphertext tdec_combine; 22x the parallelism at N=64 t=21.
 TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
                                                        const uint32_t* __restrict__ idx,
-                                                       const uint8_t* __restrict__ V,
-                                                       const uint64_t* __restrict__ V_off,
-                                                       uint8_t* __restrict__ out, int32_t* __restrict__ status) {
+                                                       uint8_t* __restrict__ seeds, int32_t* __restrict__ status) {
     const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;
     const uint32_t i = threadIdx.x & 31u, half = threadIdx.x & 32u;
     const uint32_t m = t + 1;
@@ -1178,12 +1275,7 @@ TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
     const G1A sum = g1_to_affine(acc);
     uint8_t cg[48];
     g1_compress(cg, sum);
-    uint8_t seed[32];
-    sha3_bytes(cg, 48, seed);
-    ChaChaRng rng;
-    rng.init(seed);
-    const uint64_t off = V_off[g], len = V_off[g + 1] - off;
-    for (uint64_t b = 0; b < len; ++b) out[off + b] = V[off + b] ^ (uint8_t)(rng.next_u32() & 0xFFu);
+    sha3_bytes(cg, 48, seeds + 32ull * g);  // xor_with_hash's key: the keystream runs in tdec_keystream_xor
 }
 
 // ------------------------------------------------------------------ SURVEY.md §8(f1)/(f2)
@@ -1357,45 +1449,48 @@ TDEC_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_
 }
 
 // PublicKey::encrypt_with_rng with r explicit: U = r G1, V = xor_with_hash(r PK, msg),
-// W = r hash_g1_g2(U, V).  V is written at the message's offsets.
-TDEC_KERNEL void tdec_encrypt(uint64_t n, const uint32_t* __restrict__ pk_aff, const int32_t* __restrict__ pk_status,
-                              const uint8_t* __restrict__ r32, const uint8_t* __restrict__ msg,
-                              const uint64_t* __restrict__ off, uint8_t* __restrict__ U48, uint8_t* __restrict__ V,
-                              uint8_t* __restrict__ W96, int32_t* __restrict__ err) {
+// W = r hash_g1_g2(U, V), in three launches: tdec_encrypt_u (U and the
+// keystream key SHA3(compress(r PK))), tdec_keystream_xor (V at the message's
+// offsets; SHA3(V) by tdec_v_digest when |V| > 64), tdec_encrypt_w (W).
+// est[k] != 0 (an undecodable public key): all-zero U and W, V untouched.
+TDEC_KERNEL void tdec_encrypt_u(uint64_t n, const uint32_t* __restrict__ pk_aff, const int32_t* __restrict__ pk_status,
+                                const uint8_t* __restrict__ r32, uint8_t* __restrict__ U48,
+                                uint8_t* __restrict__ W96, uint8_t* __restrict__ seeds, int32_t* __restrict__ est,
+                                int32_t* __restrict__ err) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     if (pk_status[0] != 0) {  // the public key does not decode: HBG_E_INVALID_POINT, all-zero U and W
         for (int i = 0; i < 48; ++i) U48[48ull * k + i] = 0;
         for (int i = 0; i < 96; ++i) W96[96ull * k + i] = 0;
+        est[k] = HBG_E_INVALID_POINT;
         if (k == 0) flag_error(err, HBG_E_INVALID_POINT);
         return;
     }
+    est[k] = 0;
     uint32_t r[8];
     load_scalar(r32 + 32ull * k, r);
     const G1A u = g1_to_affine(g1_mul_fr(fp_const(kG1x), fp_const(kG1y), r));
-    uint8_t* u48 = U48 + 48ull * k;
-    g1_compress(u48, u);
+    g1_compress(U48 + 48ull * k, u);
     G1A g = {fp_zero(), fp_zero(), true};
     if (pk_aff[24] == 0) g = g1_to_affine(g1_mul_fr(load_fp(pk_aff), load_fp(pk_aff + 12), r));
-    uint8_t cg[48], seed[32];
+    uint8_t cg[48];
     g1_compress(cg, g);
-    sha3_bytes(cg, 48, seed);
-    ChaChaRng rng;
-    rng.init(seed);
-    const uint64_t o = off[k], len = off[k + 1] - o;
-    for (uint64_t i = 0; i < len; ++i) V[o + i] = msg[o + i] ^ (uint8_t)(rng.next_u32() & 0xFFu);
+    sha3_bytes(cg, 48, seeds + 32ull * k);
+}
+
+TDEC_KERNEL void tdec_encrypt_w(uint64_t n, const uint8_t* __restrict__ r32, const uint8_t* __restrict__ U48,
+                                const uint8_t* __restrict__ V, const uint64_t* __restrict__ off,
+                                const uint8_t* __restrict__ vdig, const int32_t* __restrict__ est,
+                                uint8_t* __restrict__ W96) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || est[k] != 0) return;
+    uint32_t r[8];
+    load_scalar(r32 + 32ull * k, r);
     // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
-    uint8_t m[64 + 48];
-    uint32_t mlen;
-    if (len > 64) {
-        sha3_bytes(V + o, (uint32_t)len, m);
-        mlen = 32;
-    } else {
-        for (uint32_t i = 0; i < len; ++i) m[i] = V[o + i];
-        mlen = (uint32_t)len;
-    }
-    for (int i = 0; i < 48; ++i) m[mlen + i] = u48[i];
-    sha3_bytes(m, mlen + 48, seed);
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    uint8_t m[64 + 48], seed[32];
+    const uint32_t ml = hash_g1_g2_msg(V + o, len, vdig + 32ull * k, U48 + 48ull * k, m);
+    sha3_bytes(m, ml, seed);
     const G2A h = hash_g2_from_seed(seed);
     G2A w = {fp2_zero(), fp2_zero(), true};
     if (!h.inf) w = g2_to_affine(g2_mul_scalar(h.x, h.y, r));
@@ -1837,11 +1932,27 @@ static void count_mark(const char* name, hipStream_t st) {
 #else
 #define HBG_COUNT_MARK(name, st) ((void)0)
 #endif
+hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_off, uint8_t* dig, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_v_digest", st);
+    if (n == 0) return hipSuccess;
+    tdec_v_digest<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(n, V, V_off, dig);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uint8_t* in, const uint64_t* off,
+                                     uint8_t* out, const int32_t* status, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_keystream_xor", st);
+    if (n == 0) return hipSuccess;
+    tdec_keystream_xor<<<dim3((uint32_t)n), dim3(256), 0, st>>>(n, seeds, in, off, out, status);
+    return hipGetLastError();
+}
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
-                                  uint32_t* coefW, hipStream_t st) {
+                                  uint32_t* coefW, uint8_t* vdig, hipStream_t st) {
+    hipError_t e = launch_tdec_v_digest(n, V, V_off, vdig, st);
+    if (e != hipSuccess) return e;
     HBG_COUNT_MARK("tdec_ct_prepare", st);
-    tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, W96, ct_u, ct_status, coefH, coefW);
+    tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, vdig, W96, ct_u, ct_status, coefH,
+                                                              coefW);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
@@ -1993,14 +2104,17 @@ hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t
 }
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
-                               uint32_t* scratch, hipStream_t st) {
+                               uint32_t* scratch, uint8_t* seeds, hipStream_t st) {
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     if (t + 1 <= 32)
-        tdec_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status);
+        tdec_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
     else
-        tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, V, V_off, out, status, scratch);
-    return hipGetLastError();
+        tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // xor_with_hash(g, V) of every ciphertext whose combination succeeded
+    return launch_tdec_keystream_xor(n, seeds, V, V_off, out, status, st);
 }
 static dim3 grid64(uint64_t n) { return dim3((uint32_t)((n + 63) / 64)); }
 hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
@@ -2029,10 +2143,16 @@ hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const i
 }
 hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
                                const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
-                               int32_t* err, hipStream_t st) {
+                               uint8_t* seeds, uint8_t* vdig, int32_t* est, int32_t* err, hipStream_t st) {
     HBG_COUNT_MARK("tdec_encrypt", st);
     if (n == 0) return hipSuccess;
-    tdec_encrypt<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, r32, msg, off, U48, V, W96, err);
+    tdec_encrypt_u<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, r32, U48, W96, seeds, est, err);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = launch_tdec_keystream_xor(n, seeds, msg, off, V, est, st);
+    if (e == hipSuccess) e = launch_tdec_v_digest(n, V, off, vdig, st);
+    if (e != hipSuccess) return e;
+    HBG_COUNT_MARK("tdec_encrypt", st);
+    tdec_encrypt_w<<<grid64(n), dim3(64), 0, st>>>(n, r32, U48, V, off, vdig, est, W96);
     return hipGetLastError();
 }
 hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, const uint32_t* u_aff,

@@ -11,11 +11,13 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-/* Choose the share-verification schedule of hbg_tdec_verify_shares: 1 (the
- * default) batched small-exponent test with per-share fallback (public-key
- * fixed-base tables when each key verifies >= 2048 shares), 2 the same with
- * the tables always built, 0 one independent pairing check per share.  All
- * return identical bits. */
+/* Choose the share-verification schedule of hbg_tdec_verify_shares /
+ * hbg_tdec_threshold_decrypt / hbg_sig_verify_shares: 1 (the default) the
+ * batched small-exponent test with per-share fallback from 393,216 shares up
+ * and one independent pairing check per share below (public-key fixed-base
+ * tables when each key verifies >= 2048 shares), 2 batched at every size with
+ * the tables always built, 3 batched at every size, 0 one independent pairing
+ * check per share.  All return identical bits. */
 int hbg_test_set_tdec_batched(hbg_ctx *ctx, int on);
 /* Choose the schedule of hbg_rbc_encode_merkle for the (D, Q) with a
  * compile-time coding matrix: 0 (the default) rs_encode_const then

@@ -76,3 +76,34 @@ class ChaChaRng:
     def u8_stream(self, n: int) -> bytes:
         """rand ``Standard`` u8 = next_u32() as u8, one word per byte."""
         return bytes(self.next_u32() & 0xFF for _ in range(n))
+
+
+def keystream_u8(seed: bytes, n: int) -> bytes:
+    """u8_stream(n) of ChaChaRng(seed), all blocks at once with numpy (test
+    infrastructure for long contributions; checked against the scalar block
+    function in tests/test_oracle_tdec.py)."""
+    import numpy as np
+    nb = (n + 15) // 16
+    if nb == 0:
+        return b""
+    key = np.array(struct.unpack("<8I", bytes(seed)), dtype=np.uint32)
+    st = np.zeros((16, nb), dtype=np.uint32)
+    st[0], st[1], st[2], st[3] = 0x61707865, 0x3320646E, 0x79622D32, 0x6B206574
+    st[4:12] = key[:, None]
+    st[12] = np.arange(nb, dtype=np.uint64).astype(np.uint32)
+    w = st.copy()
+
+    def rotl(x, k):
+        return (x << np.uint32(k)) | (x >> np.uint32(32 - k))
+
+    def qr(a, b, c, d):
+        w[a] += w[b]; w[d] = rotl(w[d] ^ w[a], 16)
+        w[c] += w[d]; w[b] = rotl(w[b] ^ w[c], 12)
+        w[a] += w[b]; w[d] = rotl(w[d] ^ w[a], 8)
+        w[c] += w[d]; w[b] = rotl(w[b] ^ w[c], 7)
+    with np.errstate(over="ignore"):
+        for _ in range(10):
+            qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+            qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+        out = w + st
+    return (out.T.reshape(-1) & 0xFF).astype(np.uint8)[:n].tobytes()

@@ -130,7 +130,7 @@ def test_device_mode_out_of_range_share_indices():
         spk[9] = 1000            # key index out of range
         expect = np.ones(n_ct * n_pk, np.uint8)
         expect[[1, 9]] = 0
-        for batched in (1, 0):
+        for batched in (1, 3, 0):
             _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, batched))
             ok = torch.full((n_ct * n_pk,), 7, dtype=torch.uint8, device=dev)
             # asynchronous: the call succeeds, the next synchronisation point reports it once

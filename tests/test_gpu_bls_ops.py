@@ -224,10 +224,52 @@ def test_coin_share_verify_batched(seed, bad_rate):
     ctx = _lib.Context(0)
     try:
         outs = []
-        for mode in (1, 2, 0):
+        for mode in (1, 2, 3, 0):
             _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
             outs.append(th.verify_sig_shares_batch(pks, docs, items, ctx))
     finally:
         ctx.close()
     for o in outs:
         assert np.array_equal(o, expect)
+
+
+def test_long_contributions_encrypt_verify_decrypt():
+    """HoneyBadger threshold-encrypts the whole serialised contribution, so V
+    is as long as a proposal (BASELINE.json configs[4]: 1 MiB).  encrypt_with_rng
+    (U, V, W), Ciphertext::verify and PublicKeySet::decrypt for lengths around
+    the SHA3 block (136 B), the hash_g1_g2 cut (64 B) and up to 1 MiB, packed at
+    unaligned offsets: V and W equal the oracle's (vectorised keystream for V,
+    hashlib SHA3 inside hash_g1_g2), every ciphertext verifies (C oracle), and
+    the t+1-share combination returns the message."""
+    import hashlib
+
+    from oracle import chacha, corb
+    th = _th()
+    s = scenario()
+    ks, t, n = s["ks"], s["t"], len(s["pk_shares"])
+    pkp = ks.public_key()
+    pk = B.g1_compress(pkp)
+    rng = random.Random(23)
+    lens = [0, 1, 63, 64, 65, 135, 136, 137, 271, 5003, 70001, 1 << 20]
+    msgs = [bytes(rng.getrandbits(8) for _ in range(L)) if L < 100000 else
+            np.random.default_rng(5).integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+    rs = [rng.randrange(1, B.R) for _ in msgs]
+    cts = th.encrypt_batch(pk, msgs, rs)
+    for k in (0, 2, 3, 4, 6, 7, 9, 11):
+        r, L = rs[k], lens[k]
+        seed = hashlib.sha3_256(B.g1_compress(B.g1_mul(pkp, r))).digest()
+        v = bytes(a ^ b for a, b in zip(msgs[k], chacha.keystream_u8(seed, L))) if L < 100000 else \
+            (np.frombuffer(msgs[k], np.uint8) ^ np.frombuffer(chacha.keystream_u8(seed, L), np.uint8)).tobytes()
+        assert cts[k].V == v, L
+        u = B.g1_mul(B.G1, r)
+        assert cts[k].U == B.g1_compress(u), L
+        assert cts[k].W == B.g2_compress(B.g2_mul(T.hash_g1_g2(u, v), r)), L
+    assert th.ct_verify_batch(cts).all()
+    assert all(corb.ct_verify(c.U, c.V, c.W) for c in cts[-4:])
+    sks = [ks.secret_key_share(i) for i in range(n)]
+    pairs = [(c, i) for c in range(len(cts)) for i in range(t + 1)]
+    shares, st = th.decrypt_shares_batch(cts, sks, pairs)
+    assert (st == 0).all()
+    pts, st = th.combine_batch(t, cts, [[(i, shares[c * (t + 1) + i]) for i in range(t + 1)] for c in range(len(cts))])
+    assert st.tolist() == [0] * len(cts)
+    assert pts == msgs

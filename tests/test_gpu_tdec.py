@@ -281,14 +281,13 @@ def test_batched_verify_equals_per_share(bad_rate, seed):
     ctx = _lib.Context(0)
     try:
         outs = []
-        for mode in (1, 2, 0):
+        for mode in (1, 2, 3, 0):
             _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
             outs.append(th.verify_shares_batch(cts, pk, items, ctx))
     finally:
         ctx.close()
-    assert np.array_equal(outs[0], outs[2])
-    assert np.array_equal(outs[1], outs[2])
-    assert np.array_equal(outs[0], expect)
+    for o in outs:  # auto, batched + tables, batched, per share
+        assert np.array_equal(o, expect)
 
 
 def test_g1_mul_u64_and_add():

@@ -34,6 +34,12 @@ def test_chacha_rfc8439_block():
     assert w[0] == 0xE4E7F110 and w[1] == 0x15593BD1 and w[15] == 0x4E3C50A2
 
 
+def test_vectorised_keystream_matches_scalar_stream():
+    seed = bytes(range(7, 39))
+    for n in (0, 1, 15, 16, 17, 333, 1000):
+        assert chacha.keystream_u8(seed, n) == chacha.ChaChaRng(seed).u8_stream(n), n
+
+
 def test_compression_roundtrip():
     for k in (1, 2, 12345):
         p = B.g1_mul(B.G1, k)
