@@ -74,10 +74,9 @@ def parse():
                          "0 disables the TDec leg")
     ap.add_argument("--epoch-nodes", type=int, default=128,
                     help="configs[4]: one N-node HoneyBadger epoch spanning all ranks (RCCL all-gather); 0 disables")
-    ap.add_argument("--epoch-contrib", type=int, default=4096,
+    ap.add_argument("--epoch-contrib", type=int, default=1 << 20,
                     help="contribution bytes per node in the configs[4] epoch (threshold-encrypted, then broadcast; "
-                         "the ciphertext's V is processed lane-serially by encrypt / ct_prepare / combine, "
-                         "DESIGN.md §8)")
+                         "SURVEY.md §8(d) cfg 5: 1 MiB proposals)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo: CPU rehearsal)")
     ap.add_argument("--wire-msgs", type=int, default=65536,

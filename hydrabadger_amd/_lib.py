@@ -38,7 +38,8 @@ HBG_E_INVALID_SIGNATURE = -33
 HBG_E_UNKNOWN_PEER = -34
 HBG_WIRE_KIND_MESSAGE, HBG_WIRE_KIND_KEYGEN, HBG_WIRE_KIND_MAX = 7, 9, 10
 
-HBG_SHARE_NONE, HBG_SHARE_ACCEPTED, HBG_SHARE_FAULTY, HBG_SHARE_IGNORED = 0, 1, 2, 3
+HBG_SHARE_NONE, HBG_SHARE_ACCEPTED, HBG_SHARE_FAULTY, HBG_SHARE_IGNORED, HBG_SHARE_REPEAT = 0, 1, 2, 3, 4
+HBG_ARRIVAL_CIPHERTEXT = 0xFFFFFFFE
 
 HBG_MSG_VALUE, HBG_MSG_ECHO, HBG_MSG_READY, HBG_MSG_CAN_DECODE, HBG_MSG_ECHO_HASH = 0, 1, 2, 3, 4
 
@@ -81,8 +82,8 @@ SIGNATURES = {
     "hbg_tdec_verify_shares": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_ct_verify": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u32]),
     "hbg_tdec_combine": (_i, [_vp, _u32, _u32, _u8p, _vp, _u8p, _vp, _u8p, _vp, _u32]),
-    "hbg_tdec_threshold_decrypt": (_i, [_vp, _u32, _u32, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u8p, _vp, _u8p, _vp,
-                                        _u8p, _u32]),
+    "hbg_tdec_threshold_decrypt": (_i, [_vp, _u32, _u32, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u8p, _vp, _u32, _u8p,
+                                        _vp, _u8p, _u32]),
     "hbg_tdec_encrypt": (_i, [_vp, _u8p, _u64, _u8p, _u8p, _vp, _u8p, _u8p, _u8p, _u32]),
     "hbg_tdec_decrypt_shares": (_i, [_vp, _u32, _u8p, _u32, _u8p, _u64, _vp, _vp, _u8p, _vp, _u32]),
     "hbg_bls_sign": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u32]),

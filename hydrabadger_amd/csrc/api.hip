@@ -900,10 +900,11 @@ constexpr uint64_t kVerifyChunk = 131072;  // messages per bls_verify launch (G2
 
 int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_t n_ct, const uint8_t* U48,
                                const uint8_t* V, const uint64_t* V_off, const uint8_t* W96, const uint8_t* pk48,
-                               const uint8_t* share48, const uint32_t* arrival, uint8_t* plaintext, int32_t* status,
-                               uint8_t* outcome, uint32_t flags) {
+                               const uint8_t* share48, const uint32_t* arrival, uint32_t arrival_len,
+                               uint8_t* plaintext, int32_t* status, uint8_t* outcome, uint32_t flags) {
     if (!c || (n_ct && (!U48 || !V_off || !W96 || !pk48 || !share48 || !status || !outcome || n_nodes == 0)))
         return HBG_E_ARG;
+    if (arrival && (arrival_len == 0 || (uint64_t)n_ct * arrival_len >= (1ull << 31))) return HBG_E_ARG;
     if (n_ct == 0) return HBG_OK;
     if (t >= n_nodes || n_ct == 0xFFFFFFFFu || n_nodes == 0xFFFFFFFFu) return HBG_E_ARG;
     const uint64_t n = (uint64_t)n_ct * n_nodes, m = (uint64_t)t + 1;
@@ -920,7 +921,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     void *dpt, *dst, *doc;
     HBG_CHECK(stage_in(c, flags, 32, pk48, 48ull * n_nodes, &dpk));
     HBG_CHECK(stage_in(c, flags, 33, share48, 48ull * n, &dsh));
-    if (arrival) HBG_CHECK(stage_in(c, flags, 34, arrival, 4ull * n, &darr));
+    if (arrival) HBG_CHECK(stage_in(c, flags, 34, arrival, 4ull * n_ct * arrival_len, &darr));
     HBG_CHECK(stage_out(c, flags, 35, plaintext, vlen, &dpt));
     HBG_CHECK(stage_out(c, flags, 36, status, 4ull * n_ct, &dst));
     HBG_CHECK(stage_out(c, flags, 37, outcome, n, &doc));
@@ -950,7 +951,8 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     uint8_t* s48 = (uint8_t*)(sidx + m * n_ct);
     int32_t* sst = (int32_t*)(s48 + 48 * m * n_ct);
     HBG_TRY(bls::launch_tdec_select(n_ct, n_nodes, t, (const uint8_t*)ctok, (const uint8_t*)okb,
-                                    (const uint32_t*)darr, (const uint8_t*)dsh, sidx, s48, (uint8_t*)doc, sst,
+                                    (const uint32_t*)darr, arrival_len, (const uint8_t*)dsh, sidx, s48,
+                                    (uint8_t*)doc, sst,
                                     c->stream));
     // PublicKeySet::decrypt (interpolate + xor_with_hash) of the selections
     void *scr, *sds;

@@ -88,6 +88,8 @@ struct EncodeRows {
     const uint8_t* __restrict__ pay;  // MODE 1 only: this lane's payload
     uint64_t P;
     const u32x2_a4* pre;              // MODE 3 only: the D payload windows, loaded ahead (payload_window)
+    uint32_t* ring;                   // RING only: parity row 0's word of this lane's column in the LDS ring
+    uint32_t rdw;                     // RING only: dwords between consecutive parity rows of the ring
 };
 
 // MODE 2's payload window of data row J at column p0 + t (8 bytes at the
@@ -162,7 +164,8 @@ struct EncodeCtx {
 
 // Column p0 + t of every row: data words (MODE 1/2: from the payload, stored
 // to the data rows) and the Q parity words.
-template <int D, int Q, int MODE>
+// RING: the parity words also go to the fused kernel's LDS ring (r.ring).
+template <int D, int Q, int MODE, bool RING = false>
 __device__ __forceinline__ void encode_word(const EncodeRows& r) {
     EncodeCtx<D, Q, MODE> cx{r, {}};
     uint32_t acc[Q];
@@ -171,8 +174,10 @@ __device__ __forceinline__ void encode_word(const EncodeRows& r) {
     cx.prologue(std::make_integer_sequence<int, kPrefetch - 1>{});
     cx.columns(acc, std::make_integer_sequence<int, D>{});
 #pragma unroll
-    for (int k = 0; k < Q; ++k)
+    for (int k = 0; k < Q; ++k) {
         __builtin_amdgcn_raw_buffer_store_b32(acc[k], r.sh, r.vsh, (uint32_t)((uint64_t)(D + k) * r.S + 4 * r.p0), 0);
+        if constexpr (RING) r.ring[k * r.rdw] = acc[k];
+    }
 }
 
 // One thread = 4 byte positions of one instance, all N shards; one 256-thread
@@ -519,17 +524,28 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
 // phases over the same lanes:
 //   encode pass  lane = column: LPI 4-byte columns of every row of its
 //                instance (the constant-matrix split-nibble coder,
-//                encode_word), stored to the shard rows (written once);
+//                encode_word), stored to the shard rows (written once); the
+//                Q parity words also go to an LDS ring, row-major;
 //   absorb       lane = row: every 136-byte Keccak block that the passes so
-//                far have completed is read back by its row's lane and
-//                absorbed (Keccak-f, keccak_asm.h).
-// The read-back is of bytes this workgroup stored moments earlier, so it is
-// served by L2 (sc1 loads: the vector L1 may hold a stale copy of a line the
-// previous block's loads touched before the pass wrote it), not by a second
-// sweep of 25 GB through HBM as in rs_encode_const -> merkle_build.
+//                far have completed is absorbed (Keccak-f, keccak_asm.h) —
+//                parity rows read it from the LDS ring (the transpose column ->
+//                row happens in LDS, parity bytes never come back from memory),
+//                data rows from the shard rows just stored (sc1 loads served by
+//                L2: the vector L1 may hold a stale copy of a line touched
+//                before the pass wrote it).
+// Ring: R bytes per parity row, R a multiple of 136 (a block never wraps),
+// R >= one pass + the previous pass's unabsorbed tail (< 136), R/8 odd (a
+// ds_read_b64 of R-strided rows hits 64 distinct banks per 32-lane group).
+// The Keccak state stays in registers across encode passes.
 // Addressing: raw buffer resources over the workgroup's shard and payload
 // blocks, row offsets in SGPRs, the lane's offsets in VGPRs.
 // Then the leaf digests and hbbft's tree (odd node promoted) in LDS.
+__host__ __device__ constexpr uint32_t fused_ring_bytes(uint32_t pass_bytes) {
+    uint32_t r = 136;
+    while (r < pass_bytes + 135 || ((r / 8) & 1) == 0) r += 136;
+    return r;
+}
+
 template <int D, int Q>
 struct FusedShape {
     static constexpr uint32_t N = D + Q;
@@ -537,7 +553,11 @@ struct FusedShape {
     static constexpr uint32_t BLK = LPI < 64 ? 64 : LPI;
     static constexpr uint32_t IPB = BLK / LPI;
     static constexpr uint32_t NODES = merkle_nodes(N);
-    static constexpr int WPE = N <= 64 ? 3 : 2;  // waves per SIMD the register budget is sized for
+    static constexpr uint32_t R = fused_ring_bytes(4 * LPI);  // ring bytes per parity row
+    static constexpr uint32_t RING = IPB * Q * R;
+    static constexpr uint32_t TREE = IPB * NODES * 32;
+    static constexpr uint32_t LDS = RING > TREE ? RING : TREE;
+    static constexpr int WPE = 2;  // waves per SIMD the register budget is sized for
 };
 
 template <int D, int Q>
@@ -546,11 +566,10 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                        const uint8_t* __restrict__ payloads, uint64_t pstride, const uint64_t* __restrict__ plen,
                        uint8_t* __restrict__ levels) {
     using F = FusedShape<D, Q>;
-    constexpr uint32_t N = F::N, LPI = F::LPI, NODES = F::NODES;
-    // LDS: each lane's Keccak state is parked here during an encode pass (its
-    // 50 VGPRs go to the coder), then the leaf digests and tree levels
-    constexpr uint32_t kStash = F::BLK * 25, kTree = F::IPB * NODES * 4;
-    __shared__ uint64_t lds[kStash > kTree ? kStash : kTree];
+    constexpr uint32_t N = F::N, LPI = F::LPI, NODES = F::NODES, R = F::R;
+    // LDS: the parity ring [IPB][Q][R] during the sweep, then the tree levels
+    __shared__ __attribute__((aligned(16))) uint64_t lds[F::LDS / 8];
+    uint32_t* ring_all = reinterpret_cast<uint32_t*>(lds);
     uint32_t* tree_all = reinterpret_cast<uint32_t*>(lds);
     // IPB == 1: one instance per workgroup, so every instance quantity is
     // wave-uniform (SGPR bases for the encoder's row addresses)
@@ -562,17 +581,22 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     // is left unwritten (no shards, no levels)
     const bool live = inst < n && payload_fits(P, pstride, D, L);
     uint8_t* base = shards + inst * (uint64_t)N * S;
+    uint32_t* ring = ring_all + sub * (Q * R / 4);  // this instance's parity rows
     uint32_t* tree = tree_all + sub * NODES * 8;
     const uint64_t cols = (L + 3) / 4;
     const uint32_t passes = (uint32_t)((cols + LPI - 1) / LPI);
     const bool row_lane = live && t < N;
+    const bool ring_lane = row_lane && t >= (uint32_t)D;
     // buffer resources over the workgroup's first instance (uniform); a lane's
     // instance and column / row are VGPR offsets (host: IPB * N * S and
     // IPB * pstride < 2^31)
     const uint64_t inst0 = (uint64_t)blockIdx.x * F::IPB;
     EncodeRows r{raw_rsrc(shards + inst0 * N * S), raw_rsrc(payloads + inst0 * pstride),
                  (uint32_t)(sub * N * S) + 4 * t, (uint32_t)(sub * pstride) + 4 * t, S, L, 0, t, base, pay, P};
+    r.rdw = R / 4;
     const uint32_t vrow = (uint32_t)((sub * N + t) * S);  // absorb: this lane's row
+    // absorb (parity lanes): row t - D of the ring, as 8-byte words
+    const uint64_t* rrow = reinterpret_cast<const uint64_t*>(ring + (ring_lane ? t - D : 0) * (R / 4));
     u64p a[25];
     keccak_zero(a);
     uint32_t done = 0;  // 136-byte blocks absorbed (the same count for every row)
@@ -582,37 +606,43 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         const uint64_t end = 4ull * ((uint64_t)ps * LPI + LPI);  // value-byte end of the pass in a row
         return ps > 0 && end <= L && (uint64_t)(D - 1) * L + end + 4 <= P + 4;
     };
+    // one 136-byte block of this lane's row at byte 136 * done, words [0, nw)
+    auto load_block = [&](uint64_t (&w)[17]) {
+        if (ring_lane) {
+            const uint32_t rp = (136u * done) % R / 8;
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w[i] = rrow[rp + i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.sh, vrow + 8 * i, 136 * done, kBufSc1);
+                w[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+            }
+        }
+    };
     u32x2_a4 pre[D];  // the next interior pass's payload windows, loaded during this pass's Keccak work
     r.pre = pre;
     bool have_pre = false;
     for (uint32_t ps = 0; ps < passes; ++ps) {
         const uint32_t p0 = ps * LPI, p = p0 + t;  // this lane's column in the encode pass
         r.p0 = p0;
-        if (done > 0) {  // park the sponge state (nothing absorbed yet: it is zero)
-#pragma unroll
-            for (int i = 0; i < 25; ++i) lds[i * F::BLK + threadIdx.x] = ((uint64_t)a[i].hi << 32) | a[i].lo;
-        }
+        // ring position of this lane's column (wave-uniform pass start; a pass may wrap)
+        uint32_t wpos = (uint32_t)(((uint64_t)ps * 4 * LPI) % R) + 4 * t;
+        if (wpos >= R) wpos -= R;
+        r.ring = ring + wpos / 4;
         if (live) {
             if (have_pre) {
-                encode_word<D, Q, 3>(r);
+                encode_word<D, Q, 3, true>(r);
             } else if (interior(ps)) {
-                encode_word<D, Q, 2>(r);
+                encode_word<D, Q, 2, true>(r);
             } else if (4 * (uint64_t)p < L) {
-                encode_word<D, Q, 1>(r);
+                encode_word<D, Q, 1, true>(r);
             }
         }
-        // the pass's stores are complete in L2 before any lane reads them back
+        // the pass's stores are complete in L2 (data rows) and in LDS (parity
+        // rows) before any lane reads them back
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (F::BLK > 64) __syncthreads();
-        if (done > 0) {
-#pragma unroll
-            for (int i = 0; i < 25; ++i) {
-                const uint64_t v = lds[i * F::BLK + threadIdx.x];
-                a[i] = {(uint32_t)v, (uint32_t)(v >> 32)};
-            }
-        } else {
-            keccak_zero(a);
-        }
+        __syncthreads();
         const uint64_t written = 4ull * LPI * (ps + 1);
         const uint64_t avail = written < L ? written : L;
         const bool next_pre = live && ps + 1 < passes && interior(ps + 1);
@@ -628,11 +658,7 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         while ((uint64_t)(done + 1) * 136 <= avail) {
             if (row_lane) {
                 uint64_t w[17];
-#pragma unroll
-                for (int i = 0; i < 17; ++i) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.sh, vrow + 8 * i, 136 * done, kBufSc1);
-                    w[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-                }
+                load_block(w);
 #pragma unroll
                 for (int i = 0; i < 17; ++i) {
                     a[i].lo ^= (uint32_t)w[i];
@@ -646,23 +672,26 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             ++done;
         }
         prefetch();
+        // the next pass overwrites ring bytes this sweep has just absorbed
+        __syncthreads();
     }
     uint32_t d[8];
     if (row_lane) {
         // final (possibly empty) block: bytes [136 done, L) + FIPS-202 padding.
-        // Reads stay below round_up(L, 8) <= S.
+        // Reads stay below round_up(L, 8) <= S (rows) / inside the ring.
         const uint32_t rem = (uint32_t)(L - (uint64_t)done * 136);
+        uint64_t w[17];
+        load_block(w);
 #pragma unroll
         for (int i = 0; i < 17; ++i) {
-            uint64_t w = 0;
+            uint64_t v = 0;
             if ((uint32_t)(8 * i) < rem) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.sh, vrow + 8 * i, 136 * done, kBufSc1);
-                w = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                v = w[i];
                 const uint32_t left = rem - 8 * i;
-                if (left < 8) w &= ~0ull >> (64 - 8 * left);
+                if (left < 8) v &= ~0ull >> (64 - 8 * left);
             }
-            a[i].lo ^= (uint32_t)w;
-            a[i].hi ^= (uint32_t)(w >> 32);
+            a[i].lo ^= (uint32_t)v;
+            a[i].hi ^= (uint32_t)(v >> 32);
         }
         const uint32_t wi = rem >> 3, sh = (rem & 7) * 8;
 #pragma unroll
@@ -681,7 +710,7 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         }
     }
     uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)NODES * 32);
-    __syncthreads();  // the tree reuses the state stash
+    __syncthreads();  // the tree reuses the ring
     if (row_lane) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) tree[t * 8 + i] = d[i];
@@ -695,13 +724,13 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         if (live && t < nn) {
             uint32_t h[8];
             if (2 * t + 1 < cnt) {
-                uint32_t l[8], r[8];
+                uint32_t l[8], rr[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     l[i] = tree[(lbase + 2 * t) * 8 + i];
-                    r[i] = tree[(lbase + 2 * t + 1) * 8 + i];
+                    rr[i] = tree[(lbase + 2 * t + 1) * 8 + i];
                 }
-                sha3_pair<1>(l, r, h);
+                sha3_pair<1>(l, rr, h);
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) h[i] = tree[(lbase + 2 * t) * 8 + i];

@@ -96,8 +96,9 @@ hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const u
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
 hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8_t* ct_ok, const uint8_t* ok,
-                              const uint32_t* arrival, const uint8_t* share48, uint32_t* sel_idx, uint8_t* sel48,
-                              uint8_t* outcome, int32_t* sel_status, hipStream_t st);
+                              const uint32_t* arrival, uint32_t arrival_len, const uint8_t* share48,
+                              uint32_t* sel_idx, uint8_t* sel48, uint8_t* outcome, int32_t* sel_status,
+                              hipStream_t st);
 hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st);
 hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32_t* status, hipStream_t st);
 // seeds: [n][32] scratch (xor_with_hash keys, consumed by tdec_keystream_xor)

@@ -921,58 +921,106 @@ TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
 }
 
 // ---------------------------------------------------------------- ThresholdDecrypt glue (a18)
-// hbbft ThresholdDecrypt [EXT, src/threshold_decrypt.rs] for one ciphertext of
-// the epoch, given every sender's share verdict (PublicKeyShare::
-// verify_decryption_share, computed for all shares by the batched verifier):
-//  * set_ciphertext: an invalid ciphertext (Ciphertext::verify false) is
-//    rejected — no shares are processed, no output;
-//  * handle_message(sender, share), in arrival order, until terminated: an
-//    invalid share is a fault (FaultKind::UnverifiedDecryptionShareSender), a
-//    valid one is held (a second message from a held or faulty sender
-//    changes nothing);
-//  * try_output fires as soon as more than f = t shares are held: it
-//    terminates and decrypts with the held shares (the BTreeMap of senders:
-//    node-id order) — so exactly the first t+1 valid arrivals;
-//  * shares arriving after termination are ignored (never checked).
-// One thread per ciphertext.  Outputs: the t+1 selected (index, share) pairs
-// sorted by node index for hbg_tdec_combine's kernel, a per-(ct, sender)
-// outcome byte and the selection status.
+// hbbft ThresholdDecrypt [EXT, src/threshold_decrypt.rs, recalled from
+// upstream] for one ciphertext of the epoch, given every sender's share
+// verdict (PublicKeyShare::verify_decryption_share, computed for all shares
+// by the batched verifier).  The arrival list (arrival_len entries, ended by
+// the first entry >= N other than HBG_ARRIVAL_CIPHERTEXT) is replayed:
+//  * before the ciphertext marker (HoneyBadger has not output the proposal
+//    yet): handle_message holds the share unverified; a sender already held
+//    is replaced (same bytes) and faulted (MultipleDecryptionShares:
+//    HBG_SHARE_REPEAT flag);
+//  * at the marker (no marker: before the first arrival): set_ciphertext —
+//    an invalid ciphertext (Ciphertext::verify false) ends the instance;
+//    start_decryption drops the held shares that fail verification
+//    (UnverifiedDecryptionShareSender: HBG_SHARE_FAULTY), keeps the rest
+//    (HBG_SHARE_ACCEPTED) and try_output fires if more than t are held;
+//  * after it, until terminated: an invalid share is a fault, a valid one is
+//    held, a valid one from a held sender is a repeat fault; try_output fires
+//    at t+1 held;
+//  * try_output terminates and decrypts with the first t+1 held shares in
+//    node-id order (the sender BTreeMap); later arrivals are ignored
+//    (HBG_SHARE_IGNORED, never checked).
+// One thread per ciphertext (the outcome bytes double as its per-sender
+// state; kPending marks a share held before the ciphertext).  Outputs: the
+// t+1 selected (index, share) pairs sorted by node index for hbg_tdec_combine's
+// kernel, a per-(ct, sender) outcome byte and the selection status.
 __global__ __launch_bounds__(256) void tdec_select(uint32_t n_ct, uint32_t N, uint32_t t,
                                                    const uint8_t* __restrict__ ct_ok, const uint8_t* __restrict__ ok,
-                                                   const uint32_t* __restrict__ arrival,
+                                                   const uint32_t* __restrict__ arrival, uint32_t arrival_len,
                                                    const uint8_t* __restrict__ share48, uint32_t* __restrict__ sel_idx,
                                                    uint8_t* __restrict__ sel48, uint8_t* __restrict__ outcome,
                                                    int32_t* __restrict__ sel_status) {
+    constexpr uint8_t kPending = 0x80, kBase = 3;
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_ct) return;
     const uint32_t m = t + 1;
     uint8_t* oc = outcome + k * N;
     uint32_t* idx = sel_idx + k * m;
+    const uint32_t* arr = arrival ? arrival + k * (uint64_t)arrival_len : nullptr;
+    const uint32_t len = arrival ? arrival_len : N;
     for (uint32_t i = 0; i < N; ++i) oc[i] = HBG_SHARE_NONE;
-    uint32_t held = 0;
-    int32_t st = HBG_E_NOT_ENOUGH_SHARES;
-    if (!ct_ok[k]) {
-        st = HBG_E_INVALID_CIPHERTEXT;
-    } else {
-        bool term = false;
-        for (uint32_t j = 0; j < N; ++j) {
-            const uint32_t s = arrival ? arrival[k * N + j] : j;
-            if (s >= N) break;  // end of this ciphertext's arrivals
-            if (term) {
-                if (oc[s] == HBG_SHARE_NONE) oc[s] = HBG_SHARE_IGNORED;
-                continue;
-            }
-            if (oc[s] != HBG_SHARE_NONE) continue;
-            if (ok[k * N + s]) {
-                oc[s] = HBG_SHARE_ACCEPTED;
-                idx[held++] = s;
-                if (held == m) term = true;
-            } else {
-                oc[s] = HBG_SHARE_FAULTY;
-            }
+    // the list's end and whether it carries the ciphertext marker
+    uint32_t end = len;
+    bool marker = false;
+    for (uint32_t j = 0; j < len; ++j) {
+        const uint32_t s = arr ? arr[j] : j;
+        if (s == HBG_ARRIVAL_CIPHERTEXT) {
+            marker = true;
+        } else if (s >= N) {
+            end = j;
+            break;
         }
-        if (term) st = 0;
     }
+    uint32_t held = 0;
+    bool ct_set = !marker, term = false;
+    int32_t st = HBG_E_NOT_ENOUGH_SHARES;
+    const bool good_ct = ct_ok[k] != 0;
+    if (ct_set && !good_ct) st = HBG_E_INVALID_CIPHERTEXT;
+    for (uint32_t j = 0; j < end && st != HBG_E_INVALID_CIPHERTEXT; ++j) {
+        const uint32_t s = arr ? arr[j] : j;
+        if (s == HBG_ARRIVAL_CIPHERTEXT) {
+            if (ct_set) continue;
+            ct_set = true;
+            if (!good_ct) {
+                st = HBG_E_INVALID_CIPHERTEXT;
+                break;
+            }
+            for (uint32_t i = 0; i < N; ++i) {  // start_decryption: node-id order
+                if (!(oc[i] & kPending)) continue;
+                if (ok[k * N + i]) {
+                    oc[i] = (uint8_t)((oc[i] & HBG_SHARE_REPEAT) | HBG_SHARE_ACCEPTED);
+                    if (held < m) idx[held] = i;
+                    ++held;
+                } else {
+                    oc[i] = (uint8_t)((oc[i] & HBG_SHARE_REPEAT) | HBG_SHARE_FAULTY);
+                }
+            }
+            term = held >= m;
+            continue;
+        }
+        if (!ct_set) {
+            if (oc[s] & kPending) oc[s] |= HBG_SHARE_REPEAT;
+            oc[s] |= kPending;
+            continue;
+        }
+        const uint32_t base = oc[s] & kBase;
+        if (term) {
+            if (base == HBG_SHARE_NONE) oc[s] |= HBG_SHARE_IGNORED;
+            continue;
+        }
+        if (!ok[k * N + s]) {
+            oc[s] = (uint8_t)((oc[s] & HBG_SHARE_REPEAT) | HBG_SHARE_FAULTY);
+        } else if (base == HBG_SHARE_ACCEPTED) {
+            oc[s] |= HBG_SHARE_REPEAT;
+        } else {
+            oc[s] = (uint8_t)((oc[s] & HBG_SHARE_REPEAT) | HBG_SHARE_ACCEPTED);
+            idx[held++] = s;
+            term = held == m;
+        }
+    }
+    for (uint32_t i = 0; i < N; ++i) oc[i] &= (uint8_t)~kPending;  // left by an invalid ciphertext
+    if (term && st != HBG_E_INVALID_CIPHERTEXT) st = 0;
     uint32_t* dst = reinterpret_cast<uint32_t*>(sel48 + k * m * 48ull);
     if (st != 0) {  // no output: a deterministic (invalid) selection
         for (uint32_t q = 0; q < m; ++q) idx[q] = q;
@@ -2076,12 +2124,13 @@ hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const Ch
     return hipGetLastError();
 }
 hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8_t* ct_ok, const uint8_t* ok,
-                              const uint32_t* arrival, const uint8_t* share48, uint32_t* sel_idx, uint8_t* sel48,
-                              uint8_t* outcome, int32_t* sel_status, hipStream_t st) {
+                              const uint32_t* arrival, uint32_t arrival_len, const uint8_t* share48,
+                              uint32_t* sel_idx, uint8_t* sel48, uint8_t* outcome, int32_t* sel_status,
+                              hipStream_t st) {
     HBG_COUNT_MARK("tdec_select", st);
     if (n_ct == 0) return hipSuccess;
-    tdec_select<<<dim3((n_ct + 255) / 256), dim3(256), 0, st>>>(n_ct, N, t, ct_ok, ok, arrival, share48, sel_idx,
-                                                                 sel48, outcome, sel_status);
+    tdec_select<<<dim3((n_ct + 255) / 256), dim3(256), 0, st>>>(n_ct, N, t, ct_ok, ok, arrival, arrival_len, share48,
+                                                                 sel_idx, sel48, outcome, sel_status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st) {

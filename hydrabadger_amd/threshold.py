@@ -135,6 +135,8 @@ class PublicKeySet:
 # --------------------------------------------------------------------------- a18: ThresholdDecrypt glue
 SHARE_NONE, SHARE_ACCEPTED, SHARE_FAULTY, SHARE_IGNORED = (_lib.HBG_SHARE_NONE, _lib.HBG_SHARE_ACCEPTED,
                                                            _lib.HBG_SHARE_FAULTY, _lib.HBG_SHARE_IGNORED)
+SHARE_REPEAT = _lib.HBG_SHARE_REPEAT  # flag: MultipleDecryptionShares
+ARRIVAL_CIPHERTEXT = _lib.HBG_ARRIVAL_CIPHERTEXT  # arrival entry: set_ciphertext + start_decryption
 
 
 def threshold_decrypt_arrays(t: int, n_nodes: int, U, V, V_off, W, pk48, share48, arrival, plaintext, status,
@@ -142,38 +144,43 @@ def threshold_decrypt_arrays(t: int, n_nodes: int, U, V, V_off, W, pk48, share48
     """hbbft ThresholdDecrypt for a whole epoch (hbg_tdec_threshold_decrypt):
     U [n_ct][48], W [n_ct][96], V bytes at V_off [n_ct+1], pk48 [N][48],
     share48 [n_ct][N][48] (sender i's share of ct k at [k][i]), arrival
-    [n_ct][N] sender ids in arrival order or None (node order); outputs
-    plaintext (V layout), status [n_ct] i32, outcome [n_ct][N] u8.  Host
-    numpy arrays, or (device=True) CUDA tensors."""
+    [n_ct][A] u32 sender ids in arrival order (ARRIVAL_CIPHERTEXT marks the
+    ciphertext's arrival; an entry >= N otherwise ends the list) or None
+    (node order); outputs plaintext (V layout), status [n_ct] i32, outcome
+    [n_ct][N] u8.  Host numpy arrays, or (device=True) CUDA tensors."""
     n_ct = U.shape[0]
     flags = (_lib.HBG_DEVICE if device else 0) | (_lib.HBG_ASYNC if asynchronous else 0)
+    alen = 0 if arrival is None else int(arrival.shape[1])
     check(lib().hbg_tdec_threshold_decrypt((ctx or default_context()).h, t, n_nodes, n_ct, ptr(U), ptr(V),
-                                           ptr(V_off), ptr(W), ptr(pk48), ptr(share48), ptr(arrival),
+                                           ptr(V_off), ptr(W), ptr(pk48), ptr(share48), ptr(arrival), alen,
                                            ptr(plaintext), ptr(status), ptr(outcome), flags), "ThresholdDecrypt")
 
 
 def threshold_decrypt_batch(t: int, cts: list, pk_shares: list, shares: list, arrivals=None, ctx=None):
     """One node's ThresholdDecrypt instances for an epoch's ciphertexts:
     shares[k][i] = sender i's 48-B share of cts[k] (None: never sent);
-    arrivals[k] = sender ids in arrival order (None: node order).  Returns
-    (plaintexts (None where status != 0), status array, outcome [n_ct][N])."""
+    arrivals[k] = sender ids in arrival order, repeats allowed, with
+    ARRIVAL_CIPHERTEXT where the ciphertext arrives (None: every sender once
+    in node order, after the ciphertext).  Returns (plaintexts (None where
+    status != 0), status array, outcome [n_ct][N])."""
     n_ct, n = len(cts), len(pk_shares)
     if n_ct == 0:
         return [], np.zeros(0, np.int32), np.zeros((0, n), np.uint8)
     U, V, off, W = _ct_table(cts)
     pk = np.frombuffer(b"".join(bytes(p) for p in pk_shares), np.uint8).copy().reshape(n, 48)
     sh = np.zeros((n_ct, n, 48), np.uint8)
-    arr = None
-    if arrivals is not None or any(x is None for row in shares for x in row):
-        arr = np.full((n_ct, n), 0xFFFFFFFF, np.uint32)
+    sent = []
     for k in range(n_ct):
         order = list(range(n)) if arrivals is None or arrivals[k] is None else list(arrivals[k])
-        sent = [i for i in order if i < n and shares[k][i] is not None]
+        sent.append([i for i in order if i == ARRIVAL_CIPHERTEXT or (i < n and shares[k][i] is not None)])
         for i in range(n):
             if shares[k][i] is not None:
                 sh[k, i] = np.frombuffer(bytes(shares[k][i]), np.uint8)
-        if arr is not None:
-            arr[k, :len(sent)] = sent
+    arr = None
+    if arrivals is not None or any(x is None for row in shares for x in row):
+        arr = np.full((n_ct, max(1, max(len(o) + 1 for o in sent))), 0xFFFFFFFF, np.uint32)
+        for k, o in enumerate(sent):
+            arr[k, :len(o)] = o
     pt = np.zeros(max(int(off[-1]), 1), np.uint8)
     st = np.zeros(n_ct, np.int32)
     oc = np.zeros((n_ct, n), np.uint8)

@@ -191,35 +191,49 @@ int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *sha
 /* ---- hbbft ThresholdDecrypt, batched over an epoch ----
  * One node's ThresholdDecrypt instances for n_ct ciphertexts (one per
  * accepted proposal of the epoch), N = n_nodes senders each.  Per ciphertext
- * k (hbbft threshold_decrypt.rs [EXT], reached from
- * src/hydrabadger/state.rs:486-487):
- *  - set_ciphertext: Ciphertext::verify; false -> status[k] =
- *    HBG_E_INVALID_CIPHERTEXT, nothing else happens for k;
- *  - handle_message(sender, share) for the senders of arrival[k][0..] in
- *    order (an entry >= n_nodes ends the list; arrival == NULL: every sender
- *    in node order) until the instance terminates: an invalid share
- *    (PublicKeyShare::verify_decryption_share false) is a fault
- *    (FaultKind::UnverifiedDecryptionShareSender -> outcome
- *    HBG_SHARE_FAULTY), a valid one is held (HBG_SHARE_ACCEPTED);
+ * k (hbbft threshold_decrypt.rs [EXT, recalled from upstream], reached from
+ * src/hydrabadger/state.rs:486-487) the arrival list arrival[k][0 ..
+ * arrival_len) is replayed; it ends at the first entry >= n_nodes other than
+ * HBG_ARRIVAL_CIPHERTEXT (arrival == NULL: every sender once, in node order,
+ * after the ciphertext):
+ *  - entries before HBG_ARRIVAL_CIPHERTEXT arrived before HoneyBadger output
+ *    the ciphertext: handle_message holds the share unverified; a sender
+ *    already held is faulted (FaultKind::MultipleDecryptionShares ->
+ *    HBG_SHARE_REPEAT flag);
+ *  - at HBG_ARRIVAL_CIPHERTEXT (no marker: before the first entry):
+ *    set_ciphertext runs Ciphertext::verify — false -> status[k] =
+ *    HBG_E_INVALID_CIPHERTEXT and nothing else happens for k; then
+ *    start_decryption drops the held shares that fail
+ *    PublicKeyShare::verify_decryption_share
+ *    (FaultKind::UnverifiedDecryptionShareSender -> HBG_SHARE_FAULTY; the
+ *    rest HBG_SHARE_ACCEPTED) and try_output runs;
+ *  - later entries, until the instance terminates: an invalid share is a
+ *    fault (HBG_SHARE_FAULTY), a valid one is held (HBG_SHARE_ACCEPTED), a
+ *    valid one from a sender already held is a repeat fault
+ *    (HBG_SHARE_REPEAT flag);
  *  - try_output: once t+1 shares are held the instance terminates and
- *    PublicKeySet::decrypt interpolates exactly those t+1 (node-id order)
+ *    PublicKeySet::decrypt interpolates the first t+1 held (node-id order)
  *    into plaintext (the V layout); later arrivals are ignored
- *    (HBG_SHARE_IGNORED, never checked by hbbft); fewer than t+1 valid
- *    arrivals: status HBG_E_NOT_ENOUGH_SHARES (no output).
+ *    (HBG_SHARE_IGNORED, never checked by hbbft); with fewer than t+1 valid
+ *    shares status HBG_E_NOT_ENOUGH_SHARES (no output).
  * share48 [n_ct][n_nodes][48] holds sender i's share of ciphertext k at
- * [k][i] (slots of senders that never arrive are not read for the output);
- * pk48 [n_nodes][48] the public key shares; outcome [n_ct][n_nodes].
- * Every share is verified on the device (batched, as hbg_tdec_verify_shares);
- * plaintext bytes of a ciphertext with status != 0 are unspecified. */
+ * [k][i] (a repeated message carries the same share; slots of senders that
+ * never arrive are not read for the output); pk48 [n_nodes][48] the public
+ * key shares; outcome [n_ct][n_nodes] (one HBG_SHARE_* code, optionally |
+ * HBG_SHARE_REPEAT).  Every share is verified on the device (batched, as
+ * hbg_tdec_verify_shares); plaintext bytes of a ciphertext with status != 0
+ * are unspecified. */
 #define HBG_SHARE_NONE 0u     /* no message from this sender (or not processed)        */
 #define HBG_SHARE_ACCEPTED 1u /* valid, held before termination                         */
 #define HBG_SHARE_FAULTY 2u   /* invalid before termination: UnverifiedDecryptionShareSender */
 #define HBG_SHARE_IGNORED 3u  /* arrived after termination                              */
+#define HBG_SHARE_REPEAT 4u   /* flag: MultipleDecryptionShares logged for the sender   */
+#define HBG_ARRIVAL_CIPHERTEXT 0xFFFFFFFEu /* arrival entry: set_ciphertext + start_decryption */
 int hbg_tdec_threshold_decrypt(hbg_ctx *ctx, uint32_t t, uint32_t n_nodes, uint32_t n_ct,
                                const uint8_t *U48, const uint8_t *V, const uint64_t *V_off,
                                const uint8_t *W96, const uint8_t *pk48, const uint8_t *share48,
-                               const uint32_t *arrival, uint8_t *plaintext, int32_t *status,
-                               uint8_t *outcome, uint32_t flags);
+                               const uint32_t *arrival, uint32_t arrival_len, uint8_t *plaintext,
+                               int32_t *status, uint8_t *outcome, uint32_t flags);
 
 /* ---- the proposer / node side of ThresholdDecrypt ------
  * Scalars cross the boundary as 32-byte little-endian integers (an Fr value:

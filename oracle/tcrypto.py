@@ -222,44 +222,91 @@ def public_key_share(commitment: list, i: int):
 
 # ----------------------------------------------------------------------------- a18: ThresholdDecrypt glue
 SHARE_NONE, SHARE_ACCEPTED, SHARE_FAULTY, SHARE_IGNORED = 0, 1, 2, 3
+SHARE_REPEAT = 4  # flag: FaultKind::MultipleDecryptionShares logged for the sender
+ARRIVAL_CIPHERTEXT = 0xFFFFFFFE  # arrival entry: set_ciphertext + start_decryption happen here
 E_NOT_ENOUGH_SHARES, E_INVALID_CIPHERTEXT = -20, -23
 
 
 def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arrival=None):
     """One node's hbbft ThresholdDecrypt instance [EXT, hbbft
-    src/threshold_decrypt.rs], restated:
-    set_ciphertext rejects an invalid ciphertext; handle_message(sender,
-    share) in arrival order faults an invalid share
-    (UnverifiedDecryptionShareSender) and holds a valid one until try_output
-    fires with more than t held (so: the first t+1 valid arrivals), which
-    terminates the instance and decrypts with the held shares in node-id
-    order (BTreeMap); later shares are ignored.
-    shares[i]: sender i's share (G1 point or None); arrival: sender ids in
-    arrival order (None: 0..N-1).  Returns (status, plaintext or None,
-    outcome per sender)."""
+    src/threshold_decrypt.rs, recalled from upstream: parity unpinned],
+    restated.
+
+    arrival: sender ids in arrival order (None: 0..N-1 after the ciphertext);
+    the list ends at the first entry >= N other than ARRIVAL_CIPHERTEXT, the
+    point at which HoneyBadger calls set_ciphertext + start_decryption (no
+    marker: before the first arrival).
+      * handle_message before the ciphertext: the share is held unverified;
+        a sender already held is replaced (same bytes here) and faulted
+        (MultipleDecryptionShares -> SHARE_REPEAT flag);
+      * set_ciphertext: an invalid ciphertext (Ciphertext::verify false) ends
+        the instance (E_INVALID_CIPHERTEXT); start_decryption then removes
+        the held shares that fail verify_decryption_share (node-id order,
+        UnverifiedDecryptionShareSender -> SHARE_FAULTY; the others
+        SHARE_ACCEPTED) and try_output fires if more than t are held;
+      * handle_message after the ciphertext: an invalid share is a fault
+        (SHARE_FAULTY); a valid one is held (SHARE_ACCEPTED), or, if the
+        sender is already held, faulted as a repeat (SHARE_REPEAT flag);
+        try_output fires when t+1 are held;
+      * try_output terminates the instance and decrypts with the first t+1
+        held shares in node-id order (BTreeMap); later arrivals are ignored
+        unchecked (SHARE_IGNORED); fewer than t+1 valid shares:
+        E_NOT_ENOUGH_SHARES.
+    shares[i]: sender i's share (G1 point or None).  Returns (status,
+    plaintext or None, outcome per sender)."""
     n = len(pk_shares)
     order = list(range(n)) if arrival is None else list(arrival)
-    outcome = [SHARE_NONE] * n
-    if not ct.verify():
-        return E_INVALID_CIPHERTEXT, None, outcome
-    h = hash_g1_g2(ct.U, ct.V)
-    held = {}
-    for s in order:
-        if s >= n:
+    for j, s in enumerate(order):
+        if s >= n and s != ARRIVAL_CIPHERTEXT:
+            order = order[:j]
             break
-        if len(held) == t + 1:
-            if outcome[s] == SHARE_NONE:
-                outcome[s] = SHARE_IGNORED
+    outcome = [SHARE_NONE] * n
+    ct_ok = ct.verify()
+    h = hash_g1_g2(ct.U, ct.V) if ct_ok else None
+
+    def valid(s):
+        return shares[s] is not None and verify_decryption_share(pk_shares[s], shares[s], ct, h)
+
+    ct_set = ARRIVAL_CIPHERTEXT not in order
+    if ct_set and not ct_ok:
+        return E_INVALID_CIPHERTEXT, None, outcome
+    pending, held, term = set(), set(), False
+    for s in order:
+        if s == ARRIVAL_CIPHERTEXT:
+            if ct_set:
+                continue
+            ct_set = True
+            if not ct_ok:
+                return E_INVALID_CIPHERTEXT, None, outcome
+            for p in sorted(pending):
+                if valid(p):
+                    outcome[p] |= SHARE_ACCEPTED
+                    held.add(p)
+                else:
+                    outcome[p] |= SHARE_FAULTY
+            pending.clear()
+            term = len(held) >= t + 1
             continue
-        if outcome[s] != SHARE_NONE:
+        if not ct_set:
+            if s in pending:
+                outcome[s] |= SHARE_REPEAT
+            pending.add(s)
             continue
-        sh = shares[s]
-        valid = sh is not None and verify_decryption_share(pk_shares[s], sh, ct, h)
-        if valid:
-            outcome[s] = SHARE_ACCEPTED
-            held[s] = sh
-        else:
-            outcome[s] = SHARE_FAULTY
-    if len(held) < t + 1:
+        base = outcome[s] & 3
+        if term:
+            if base == SHARE_NONE:
+                outcome[s] |= SHARE_IGNORED
+            continue
+        if not valid(s):
+            outcome[s] = (outcome[s] & SHARE_REPEAT) | SHARE_FAULTY
+            continue
+        if s in held:
+            outcome[s] |= SHARE_REPEAT
+            continue
+        held.add(s)
+        outcome[s] = (outcome[s] & SHARE_REPEAT) | SHARE_ACCEPTED
+        term = len(held) == t + 1
+    if not term:
         return E_NOT_ENOUGH_SHARES, None, outcome
-    return 0, decrypt(t, sorted(held.items()), ct), outcome
+    sel = sorted(held)[: t + 1]
+    return 0, decrypt(t, [(i, shares[i]) for i in sel], ct), outcome

@@ -46,6 +46,8 @@ pub const HBG_SHARE_NONE: u8 = 0;
 pub const HBG_SHARE_ACCEPTED: u8 = 1;
 pub const HBG_SHARE_FAULTY: u8 = 2;
 pub const HBG_SHARE_IGNORED: u8 = 3;
+pub const HBG_SHARE_REPEAT: u8 = 4;
+pub const HBG_ARRIVAL_CIPHERTEXT: u32 = 0xFFFF_FFFE;
 pub const HBG_MSG_VALUE: u32 = 0;
 pub const HBG_MSG_ECHO: u32 = 1;
 pub const HBG_MSG_READY: u32 = 2;
@@ -96,8 +98,9 @@ extern "C" {
                             flags: u32) -> c_int;
     pub fn hbg_tdec_threshold_decrypt(ctx: *mut hbg_ctx, t: u32, n_nodes: u32, n_ct: u32, u48: *const u8,
                                       v: *const u8, v_off: *const u64, w96: *const u8, pk48: *const u8,
-                                      share48: *const u8, arrival: *const u32, plaintext: *mut u8,
-                                      status: *mut i32, outcome: *mut u8, flags: u32) -> c_int;
+                                      share48: *const u8, arrival: *const u32, arrival_len: u32,
+                                      plaintext: *mut u8, status: *mut i32, outcome: *mut u8,
+                                      flags: u32) -> c_int;
     pub fn hbg_tdec_encrypt(ctx: *mut hbg_ctx, pk48: *const u8, n: u64, r32: *const u8, msg: *const u8,
                             msg_off: *const u64, u48: *mut u8, v: *mut u8, w96: *mut u8, flags: u32) -> c_int;
     pub fn hbg_tdec_decrypt_shares(ctx: *mut hbg_ctx, n_ct: u32, u48: *const u8, n_sk: u32, sk32: *const u8,

@@ -170,9 +170,11 @@ impl Engine {
 
     /// hbbft ThresholdDecrypt for an epoch (hbg_tdec_threshold_decrypt):
     /// `cts[k] = (U48, V, W96)`, `shares[k][i]` = sender i's share of ct k
-    /// (None: never arrived), `arrival[k]` = sender order (None: node order).
-    /// Returns per ciphertext `Ok(plaintext)` or the status code, and the
-    /// per-sender outcomes (HBG_SHARE_*).
+    /// (None: never arrived), `arrival[k]` = sender order, repeats allowed,
+    /// with `HBG_ARRIVAL_CIPHERTEXT` where the ciphertext arrives (None: node
+    /// order, after the ciphertext).  Returns per ciphertext `Ok(plaintext)`
+    /// or the status code, and the per-sender outcomes (HBG_SHARE_*, possibly
+    /// | HBG_SHARE_REPEAT).
     #[allow(clippy::type_complexity)]
     pub fn threshold_decrypt(&self, t: u32, pk_shares: &[[u8; 48]], cts: &[([u8; 48], Vec<u8>, [u8; 96])],
                              shares: &[Vec<Option<[u8; 48]>>], arrival: Option<&[Vec<u32>]>)
@@ -190,22 +192,26 @@ impl Engine {
             off[k + 1] = v.len() as u64;
         }
         let mut sh = vec![0u8; 48 * n * n_ct];
-        let mut arr = vec![u32::MAX; n * n_ct];
+        // the arrivals that reach the instance (senders that sent a share, and the marker)
+        let mut sent: Vec<Vec<u32>> = Vec::with_capacity(n_ct);
         for k in 0..n_ct {
             let order: Vec<u32> = match arrival {
                 Some(a) => a[k].clone(),
                 None => (0..n as u32).collect(),
             };
-            let mut j = 0;
-            for s in order {
-                if (s as usize) < n {
-                    if let Some(x) = shares[k][s as usize] {
-                        sh[48 * (k * n + s as usize)..48 * (k * n + s as usize + 1)].copy_from_slice(&x);
-                        arr[k * n + j] = s;
-                        j += 1;
-                    }
+            for (i, x) in shares[k].iter().enumerate() {
+                if let Some(x) = x {
+                    sh[48 * (k * n + i)..48 * (k * n + i + 1)].copy_from_slice(x);
                 }
             }
+            sent.push(order.into_iter()
+                .filter(|&s| s == HBG_ARRIVAL_CIPHERTEXT || ((s as usize) < n && shares[k][s as usize].is_some()))
+                .collect());
+        }
+        let alen = sent.iter().map(|o| o.len() + 1).max().unwrap_or(1);
+        let mut arr = vec![u32::MAX; alen * n_ct];
+        for (k, o) in sent.iter().enumerate() {
+            arr[k * alen..k * alen + o.len()].copy_from_slice(o);
         }
         let pk: Vec<u8> = pk_shares.iter().flat_map(|p| p.iter().copied()).collect();
         let mut pt = vec![0u8; v.len().max(1)];
@@ -213,8 +219,8 @@ impl Engine {
         let mut outcome = vec![0u8; n * n_ct];
         self.with(|c| check(unsafe {
             hbg_tdec_threshold_decrypt(c, t, n as u32, n_ct as u32, u.as_ptr(), v.as_ptr(), off.as_ptr(),
-                                       w.as_ptr(), pk.as_ptr(), sh.as_ptr(), arr.as_ptr(), pt.as_mut_ptr(),
-                                       status.as_mut_ptr(), outcome.as_mut_ptr(), 0)
+                                       w.as_ptr(), pk.as_ptr(), sh.as_ptr(), arr.as_ptr(), alen as u32,
+                                       pt.as_mut_ptr(), status.as_mut_ptr(), outcome.as_mut_ptr(), 0)
         }))?;
         let out = (0..n_ct)
             .map(|k| if status[k] == 0 {

@@ -68,9 +68,9 @@ def rust_prototypes() -> dict:
 
 
 def _eval_const(expr: str) -> int:
-    expr = re.sub(r"(\d+)u\b", r"\1", expr.strip())
-    assert re.fullmatch(r"[\d\s\(\)\*\+\-]+", expr), expr
-    return int(eval(expr))  # digits and arithmetic only (asserted above)
+    expr = re.sub(r"\b(0[xX][0-9a-fA-F]+|\d+)[uU]\b", r"\1", expr.strip())
+    assert re.fullmatch(r"(0[xX][0-9a-fA-F]+|[\d\s\(\)\*\+\-])+", expr), expr
+    return int(eval(expr))  # integer literals and arithmetic only (asserted above)
 
 
 def header_constants() -> dict:

@@ -19,7 +19,7 @@ from oracle import bls12_381 as B
 from oracle import tcrypto as T
 from tests import tdec_fixtures as fx
 
-ACC, FLT, IGN, NONE = T.SHARE_ACCEPTED, T.SHARE_FAULTY, T.SHARE_IGNORED, T.SHARE_NONE
+ACC, FLT, IGN, NONE, REP = T.SHARE_ACCEPTED, T.SHARE_FAULTY, T.SHARE_IGNORED, T.SHARE_NONE, T.SHARE_REPEAT
 
 
 def _case(seed=5):
@@ -39,10 +39,42 @@ def test_oracle_first_t_plus_one_valid_arrivals():
     st, pt, oc = T.threshold_decrypt(t, ct, pks, shares)
     assert st == 0 and pt == sc["msgs"][0]
     assert oc == [ACC, FLT, ACC, ACC, IGN, IGN, IGN]
-    # arrival order decides which shares are held; a repeated sender changes nothing
+    # arrival order decides which shares are held; a held sender's second
+    # message is a MultipleDecryptionShares fault and adds nothing
     st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[6, 6, 1, 5, 0, 3, 2])
     assert st == 0 and pt == sc["msgs"][0]
-    assert oc == [ACC, FLT, IGN, IGN, NONE, ACC, ACC]
+    assert oc == [ACC, FLT, IGN, IGN, NONE, ACC, ACC | REP]
+    # a faulty sender's second message is faulted again; after termination nothing is checked
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[1, 0, 1, 2, 3, 3, 1])
+    assert st == 0 and oc == [ACC, FLT, ACC, ACC, NONE, NONE, NONE]
+
+
+def test_oracle_shares_before_the_ciphertext():
+    """Shares that arrive before HoneyBadger outputs the ciphertext are held
+    unverified (a repeat is faulted at once); start_decryption drops the
+    invalid ones and try_output fires on what is left."""
+    sc = _case()
+    t, ct, pks = sc["t"], sc["cts"][0], sc["pk_shares"]
+    shares = list(sc["shares"][0])
+    shares[1] = B.g1_add(shares[1], B.G1)
+    M = T.ARRIVAL_CIPHERTEXT
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[3, 1, 3, M, 0, 2, 4])
+    assert st == 0 and pt == sc["msgs"][0]
+    assert oc == [ACC, FLT, ACC, ACC | REP, IGN, NONE, NONE]
+    # more than t+1 valid before the ciphertext: output at once with the first t+1 by node id
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[5, 4, 6, 0, M, 1, 2])
+    assert st == 0 and pt == sc["msgs"][0]
+    assert oc == [ACC, IGN, IGN, NONE, ACC, ACC, ACC]
+    # a second marker changes nothing; no marker = the ciphertext came first
+    assert T.threshold_decrypt(t, ct, pks, shares, arrival=[M, 0, M, 2, 3]) == \
+        T.threshold_decrypt(t, ct, pks, shares, arrival=[0, 2, 3])
+    # an invalid ciphertext ends the instance at the marker (repeat faults already logged stay)
+    bad_ct = T.Ciphertext(ct.U, ct.V, B.g2_mul(ct.W, 2))
+    st, pt, oc = T.threshold_decrypt(t, bad_ct, pks, shares, arrival=[0, 0, M, 2, 3])
+    assert st == T.E_INVALID_CIPHERTEXT and pt is None and oc == [REP] + [NONE] * 6
+    # too few valid shares by the end of the list
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[1, 0, M, 1, 2])
+    assert st == T.E_NOT_ENOUGH_SHARES and oc == [ACC, FLT, ACC, NONE, NONE, NONE, NONE]
 
 
 def test_oracle_not_enough_and_invalid_ciphertext():
@@ -82,11 +114,15 @@ def test_gpu_glue_matches_oracle_hand_cases():
     cts = [ct0, ct0, ct1, bad_ct]
     sh = [list(sc["shares"][0]), list(sc["shares"][0]), list(sc["shares"][1]), list(sc["shares"][2])]
     sh[1][1] = B.g1_add(sh[1][1], B.G1)
-    arrivals = [None, [6, 6, 1, 5, 0, 3, 2], [0, 4], None]
+    M = T.ARRIVAL_CIPHERTEXT
+    cts += [ct0, ct0, bad_ct, ct1]
+    sh += [list(sh[1]), list(sh[1]), list(sc["shares"][2]), list(sc["shares"][1])]
+    arrivals = [None, [6, 6, 1, 5, 0, 3, 2], [0, 4], None,
+                [3, 1, 3, M, 0, 2, 4], [5, 4, 6, 0, M, 1, 2], [0, 0, M, 2, 3], [1, 0, 1, M, 1, 2, 2, 5]]
     pts, st, oc = th.threshold_decrypt_batch(
         t, [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in cts], pks,
         [[B.g1_compress(x) for x in row] for row in sh], arrivals)
-    for k in range(4):
+    for k in range(len(cts)):
         rst, rpt, roc = T.threshold_decrypt(t, cts[k], sc["pk_shares"], sh[k], arrivals[k])
         assert st[k] == rst and list(oc[k]) == roc and pts[k] == rpt, k
 
@@ -123,6 +159,38 @@ def test_gpu_glue_random_epochs_match_oracle(seed):
         rst, rpt, roc = T.threshold_decrypt(t, sc["cts"][k], sc["pk_shares"], shares[k], arrivals[k])
         assert (int(st[k]), list(oc[k]), pts[k]) == (rst, roc, rpt), k
     assert int(st[5]) == T.E_NOT_ENOUGH_SHARES
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 4])
+def test_gpu_glue_early_shares_and_repeats_match_oracle(seed):
+    """HoneyBadger-style arrivals: the ciphertext marker at a seeded position
+    (shares before it held unverified), ~20 % of the messages repeated
+    (MultipleDecryptionShares), ~15 % of the shares corrupted."""
+    th = _th()
+    rng = random.Random(seed)
+    sc = fx.scenario(16, 12, 48, seed=30 + seed)
+    t, n, n_ct = sc["t"], 16, 12
+    M = T.ARRIVAL_CIPHERTEXT
+    shares, arrivals = [], []
+    for k in range(n_ct):
+        shares.append([_corrupt(rng.randrange(3), k, i, sc, rng) if rng.random() < 0.15 else sc["shares"][k][i]
+                       for i in range(n)])
+        order = list(range(n))
+        rng.shuffle(order)
+        order += [rng.randrange(n) for _ in range(rng.randrange(0, 5))]
+        rng.shuffle(order)
+        order.insert(rng.randrange(0, len(order) + 1), M)
+        arrivals.append(order)
+    cts = [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in sc["cts"]]
+    pts, st, oc = th.threshold_decrypt_batch(t, cts, [B.g1_compress(p) for p in sc["pk_shares"]],
+                                             [[B.g1_compress(x) for x in row] for row in shares], arrivals)
+    flags = 0
+    for k in range(n_ct):
+        rst, rpt, roc = T.threshold_decrypt(t, sc["cts"][k], sc["pk_shares"], shares[k], arrivals[k])
+        assert (int(st[k]), list(oc[k]), pts[k]) == (rst, roc, rpt), k
+        flags += sum(1 for x in roc if x & REP)
+    assert flags > 0
 
 
 @pytest.mark.gpu
@@ -254,3 +322,43 @@ def test_configs3_size_threshold_decrypt_100k():
     ph = pt.cpu().numpy()
     assert rst.tolist() == [0] * len(sample)
     assert pts == [ph[L * k:L * (k + 1)].tobytes() for k in sample]
+
+
+# ------------------------------------------------------------------ a18 fixture (tests/golden/tdec_golden.json)
+def _a18_fixture():
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tdec_golden.json")))
+    sc = g["scenario"]
+    M = T.ARRIVAL_CIPHERTEXT
+    cases = []
+    for c in g["threshold_decrypt"]["cases"]:
+        ct = sc["cts"][c["ct"]]
+        shares = [bytes.fromhex(x) for x in ct["shares"]]
+        shares[c["bad_sender"]] = bytes.fromhex(c["bad_share"])
+        arrival = [M if a == "ct" else a for a in c["arrival"]]
+        cases.append((ct, shares, arrival, c))
+    return sc, cases
+
+
+def test_oracle_matches_a18_fixture():
+    sc, cases = _a18_fixture()
+    pks = [B.g1_decompress(bytes.fromhex(p)) for p in sc["pk_shares"]]
+    for ct, shares, arrival, c in cases:
+        cto = T.Ciphertext(B.g1_decompress(bytes.fromhex(ct["U"])), bytes.fromhex(ct["V"]),
+                           B.g2_decompress(bytes.fromhex(ct["W"])))
+        st, pt, oc = T.threshold_decrypt(sc["t"], cto, pks, [B.g1_decompress(s) for s in shares], arrival)
+        assert (st, oc, None if pt is None else pt.hex()) == (c["status"], c["outcome"], c["plaintext"])
+
+
+@pytest.mark.gpu
+def test_gpu_glue_matches_a18_fixture():
+    th = _th()
+    sc, cases = _a18_fixture()
+    cts = [th.Ciphertext(bytes.fromhex(ct["U"]), bytes.fromhex(ct["V"]), bytes.fromhex(ct["W"]))
+           for ct, _, _, _ in cases]
+    pts, st, oc = th.threshold_decrypt_batch(sc["t"], cts, [bytes.fromhex(p) for p in sc["pk_shares"]],
+                                             [s for _, s, _, _ in cases], [a for _, _, a, _ in cases])
+    for k, (_, _, _, c) in enumerate(cases):
+        assert (int(st[k]), list(oc[k]), None if pts[k] is None else pts[k].hex()) == \
+            (c["status"], c["outcome"], c["plaintext"]), k
