@@ -185,6 +185,50 @@ def fp_per_share(prof: dict, key: str, n_shares: int) -> float:
     return total
 
 
+# Kernels of one hbg_tdec_threshold_decrypt call (the epoch generator's
+# encrypt / decrypt_share kernels in the same profile are not part of it).
+TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_prepare", "tdec_ct_verify", "tdec_pair_index", "tdec_pk_table",
+                       "tdec_iota", "tdec_group_marks", "tdec_batch_heads", "tdec_batch_desc", "tdec_batch_leaves",
+                       "tdec_batch_check", "tdec_verify_shares", "tdec_select", "tdec_combine_grp",
+                       "tdec_status_merge", "tdec_index_sanitize")
+
+
+def tdec_pmc_traffic(n_shares: int) -> dict:
+    """HBM bytes of one ThresholdDecrypt call at the bench shape (100k x 64,
+    1 % bad), from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE per kernel, profiles/r03/pmc_tdec_100k.json); almost all of it
+    is the kernels' scratch (spill / call-frame) traffic, since a share is 48 B."""
+    path = os.path.join(ROOT, "profiles", "r03", "pmc_tdec_100k.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    per_kernel = {}
+    for name, v in d.items():
+        short = name.split("::")[-1]
+        if short in TDEC_DRIVER_KERNELS and isinstance(v, dict) and "hbm_read_bytes_corrected" in v:
+            per_kernel[short] = v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
+    if not per_kernel or n_shares != 6_400_000:
+        return {}
+    total = sum(per_kernel.values())
+    return {"bytes_per_call": total, "bytes_per_share": total / n_shares,
+            "per_kernel_bytes_per_share": {k: v / n_shares for k, v in sorted(per_kernel.items(), key=lambda x: -x[1])},
+            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                      "passes over tools/tdec_kbench.py --cts 100000)"}
+
+
+def fp_count_floor() -> dict:
+    """The batched verifier's executed Fp count with no bad share (no group
+    testing, no per-share fallback): profiles/r03/fpcount_batched_0pct.json."""
+    path = os.path.join(ROOT, "profiles", "r03", "fpcount_batched_0pct.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    return {"per_share_total": d["per_share_total"], "per_share_verify_total": d["per_share_verify_total"],
+            "source": os.path.relpath(path, ROOT)}
+
+
 def kernel_meta(names) -> dict:
     """VGPR / scratch / waves-per-SIMD of the named kernels (tools/kernel_meta.py)."""
     try:
@@ -194,7 +238,7 @@ def kernel_meta(names) -> dict:
     out = {}
     for mangled, v in k.items():
         for n in names:
-            if f"{len(n)}{n}E" in mangled:
+            if f"{len(n)}{n}E" in mangled or f"{len(n)}{n}I" in mangled:
                 out[n] = {x: v[x] for x in ("vgpr", "agpr", "sgpr", "scratch_bytes", "lds_bytes",
                                             "waves_per_simd_by_regs")}
     return out
@@ -314,6 +358,20 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             "occupancy": kernel_meta(["tdec_batch_leaves", "tdec_batch_check", "tdec_verify_shares",
                                       "tdec_ct_prepare", "tdec_ct_verify", "tdec_combine_grp"]),
         }
+        floor = fp_count_floor()
+        if floor:
+            # executed count at this bad-share rate vs the same algorithm with no bad share
+            out["roofline"]["fp_mul_per_share_no_bad_shares"] = floor["per_share_total"]
+            out["roofline"]["executed_vs_no_bad_shares"] = per_share / floor["per_share_total"]
+            out["roofline"]["verify_only"]["executed_vs_no_bad_shares"] = per_share_v / floor["per_share_verify_total"]
+            out["roofline"]["floor_source"] = floor["source"]
+        tr = tdec_pmc_traffic(n)
+        if tr:
+            out["roofline"]["traffic"] = tr["bytes_per_call"]
+            out["roofline"]["traffic_unit"] = "HBM bytes per hbg_tdec_threshold_decrypt call (PMC)"
+            out["roofline"]["traffic_per_share"] = tr["bytes_per_share"]
+            out["roofline"]["traffic_per_share_by_kernel"] = tr["per_kernel_bytes_per_share"]
+            out["roofline"]["traffic_source"] = tr["source"]
     return out, ep
 
 

@@ -32,11 +32,15 @@ def _deps_mtime(src: str) -> float:
 
 def _compile(src: str, force: bool) -> str:
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
-    if force or not os.path.exists(obj) or os.path.getmtime(obj) < _deps_mtime(src):
+    deps = _deps_mtime(src)
+    if force or not os.path.exists(obj) or os.path.getmtime(obj) < deps:
         cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+        # stamp the object with its inputs' time: an edit made while hipcc ran
+        # still marks it stale
+        os.utime(obj, (deps, deps))
     return obj
 
 

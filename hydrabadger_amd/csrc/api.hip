@@ -1072,7 +1072,7 @@ int hbg_sig_combine(hbg_ctx* c, uint32_t t, uint64_t n, const uint8_t* share96, 
                     uint8_t* sig96, uint8_t* parity, int32_t* status, uint32_t flags) {
     if (!c || (n && (!share96 || !share_index || !sig96 || !parity || !status))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    if (t >= 32) return HBG_E_ARG;  // one 32-lane group per coin: t + 1 <= 32
+    if (t >= 64) return HBG_E_ARG;  // one 32- or 64-lane group per coin: t + 1 <= 64
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t m = (uint64_t)t + 1;

@@ -1273,17 +1273,21 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
     return r;
 }
 
-// PublicKeySet::decrypt with one 32-lane group per ciphertext (t + 1 <= 32):
-// lane i owns share i — DuplicateEntry / decode checks, its Lagrange
-// coefficient lambda_i (one Fr inversion per lane) and [lambda_i] S_i — then a
-// 5-level butterfly sums the group and lane 0 hashes and XORs.  Same sum, same
-// error precedence (DuplicateEntry before an undecodable share) as the
-// one-lane-per-ciphertext tdec_combine; 22x the parallelism at N=64 t=21.
+// PublicKeySet::decrypt with one G-lane group per ciphertext (t + 1 <= G;
+// G = 32: two ciphertexts per wave, G = 64: one): lane i owns share i —
+// DuplicateEntry / decode checks, its Lagrange coefficient lambda_i (one Fr
+// inversion per lane) and [lambda_i] S_i — then a log2(G)-level butterfly
+// sums the group and lane 0 hashes (the keystream XOR runs in
+// tdec_keystream_xor).  Same sum, same error precedence (DuplicateEntry
+// before an undecodable share) as the one-lane-per-ciphertext tdec_combine
+// (kept for t + 1 > 64); 22x the parallelism at N=64 t=21, 43x at N=128 t=42.
+template <int G>
 TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
-                                                       const uint32_t* __restrict__ idx,
-                                                       uint8_t* __restrict__ seeds, int32_t* __restrict__ status) {
-    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;
-    const uint32_t i = threadIdx.x & 31u, half = threadIdx.x & 32u;
+                                  const uint32_t* __restrict__ idx, uint8_t* __restrict__ seeds,
+                                  int32_t* __restrict__ status) {
+    static_assert(G == 32 || G == 64, "group = half or whole wave");
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const uint32_t i = threadIdx.x & (G - 1), half = threadIdx.x & 32u & (uint32_t)(64 - G);
     const uint32_t m = t + 1;
     const bool live = g < n;  // no early return: the group shuffles below need every lane
     const bool act = live && i < m;
@@ -1295,8 +1299,9 @@ TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
     G1A p = {fp_zero(), fp_zero(), true};
     bool bad = false;
     if (act) bad = !g1_decompress(share48 + ((uint64_t)g * m + i) * 48, p, false);
-    const uint32_t any_dup = (uint32_t)(__ballot(dup) >> half);
-    const uint32_t any_bad = (uint32_t)(__ballot(bad) >> half);
+    const uint64_t gmask = G == 64 ? ~0ull : 0xFFFFFFFFull;
+    const bool any_dup = (__ballot(dup) >> half) & gmask;
+    const bool any_bad = (__ballot(bad) >> half) & gmask;
     const int32_t st = any_dup ? HBG_E_DUPLICATE_ENTRY : (any_bad ? HBG_E_INVALID_POINT : 0);
     G1 acc = {fp_one(), fp_one(), fp_zero()};
     if (act && st == 0 && !p.inf) {
@@ -1316,7 +1321,7 @@ TDEC_KERNEL void tdec_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
         acc = g1_mul_fr(p.x, p.y, lw);
     }
 #pragma unroll 1
-    for (int s = 1; s < 32; s <<= 1) acc = g1_add(acc, g1_shfl_xor(acc, s));
+    for (int s = 1; s < G; s <<= 1) acc = g1_add(acc, g1_shfl_xor(acc, s));
     if (!live || i != 0) return;
     status[g] = st;
     if (st != 0) return;
@@ -1591,11 +1596,13 @@ BD G2 g2_shfl_xor(const G2& p, int m) {
     return r;
 }
 
+template <int G>
 TDEC_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share96,
                                   const uint32_t* __restrict__ idx, uint8_t* __restrict__ sig96,
                                   uint8_t* __restrict__ parity, int32_t* __restrict__ status) {
-    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;
-    const uint32_t i = threadIdx.x & 31u, half = threadIdx.x & 32u;
+    static_assert(G == 32 || G == 64, "group = half or whole wave");
+    const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const uint32_t i = threadIdx.x & (G - 1), half = threadIdx.x & 32u & (uint32_t)(64 - G);
     const uint32_t m = t + 1;
     const bool live = g < n;  // no early return: the group shuffles below need every lane
     const bool act = live && i < m;
@@ -1607,8 +1614,9 @@ TDEC_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
     G2A p = {fp2_zero(), fp2_zero(), true};
     bool bad = false;
     if (act) bad = !g2_decompress(share96 + ((uint64_t)g * m + i) * 96, p, false);
-    const uint32_t any_dup = (uint32_t)(__ballot(dup) >> half);
-    const uint32_t any_bad = (uint32_t)(__ballot(bad) >> half);
+    const uint64_t gmask = G == 64 ? ~0ull : 0xFFFFFFFFull;
+    const bool any_dup = (__ballot(dup) >> half) & gmask;
+    const bool any_bad = (__ballot(bad) >> half) & gmask;
     const int32_t st = any_dup ? HBG_E_DUPLICATE_ENTRY : (any_bad ? HBG_E_INVALID_POINT : 0);
     G2 acc = {fp2_one(), fp2_one(), fp2_zero()};
     if (act && st == 0 && !p.inf) {
@@ -1627,7 +1635,7 @@ TDEC_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restr
         acc = g2_mul_scalar(p.x, p.y, lw);
     }
 #pragma unroll 1
-    for (int s = 1; s < 32; s <<= 1) acc = g2_add(acc, g2_shfl_xor(acc, s));
+    for (int s = 1; s < G; s <<= 1) acc = g2_add(acc, g2_shfl_xor(acc, s));
     if (!live || i != 0) return;
     status[g] = st;
     if (st != 0) return;
@@ -2157,7 +2165,9 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     if (t + 1 <= 32)
-        tdec_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
+        tdec_combine_grp<32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
+    else if (t + 1 <= 64)
+        tdec_combine_grp<64><<<dim3(n), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
     else
         tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, scratch);
     hipError_t e = hipGetLastError();
@@ -2218,8 +2228,11 @@ hipError_t launch_coin_combine(uint32_t n, uint32_t t, const uint8_t* share96, c
                                uint8_t* parity, int32_t* status, hipStream_t st) {
     HBG_COUNT_MARK("coin_combine", st);
     if (n == 0) return hipSuccess;
-    if (t + 1 > 32) return hipErrorInvalidValue;
-    coin_combine_grp<<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share96, idx, sig96, parity, status);
+    if (t + 1 > 64) return hipErrorInvalidValue;
+    if (t + 1 <= 32)
+        coin_combine_grp<32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share96, idx, sig96, parity, status);
+    else
+        coin_combine_grp<64><<<dim3(n), dim3(64), 0, st>>>(n, t, share96, idx, sig96, parity, status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,

@@ -286,8 +286,8 @@ int hbg_bls_verify(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
  * share) items in iterator order (share96 [n][t+1][96], share_index
  * [n][t+1]; x = index + 1) -> sig96[k] = PublicKeySet::combine_signatures,
  * parity[k] = Signature::parity() (the coin value).  status[k] = 0,
- * HBG_E_DUPLICATE_ENTRY or HBG_E_INVALID_POINT.  t + 1 <= 32 (HBG_E_ARG
- * otherwise).  Replaces hbbft ThresholdSign::try_output (reached from
+ * HBG_E_DUPLICATE_ENTRY or HBG_E_INVALID_POINT.  t + 1 <= 64 (HBG_E_ARG
+ * otherwise: one wave per coin, lane = share).  Replaces hbbft ThresholdSign::try_output (reached from
  * src/hydrabadger/state.rs:487 via BinaryAgreement's coin). */
 int hbg_sig_combine(hbg_ctx *ctx, uint32_t t, uint64_t n, const uint8_t *share96,
                     const uint32_t *share_index, uint8_t *sig96, uint8_t *parity,

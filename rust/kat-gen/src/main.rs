@@ -13,7 +13,24 @@
 //!    root and `Message::Ready(root)`;
 //!  * frames_golden.json: `SecretKey` from the fixture scalars, its public key
 //!    and `sign(message)` bytes (f2, and hash_g2 through sign);
-//!  * tdec_golden.json `hash_g2`: `SecretKey(1).sign(msg)` = hash_g2(msg) (a13).
+//!  * tdec_golden.json `hash_g2`: `SecretKey(1).sign(msg)` = hash_g2(msg) (a13);
+//!  * tdec_golden.json scenario: the key polynomial -> `PublicKeySet` (its
+//!    public key shares = the fixture's, which pins the share index
+//!    convention), `Ciphertext::verify` of every fixture ciphertext,
+//!    `verify_decryption_share` of every fixture share (and of each share
+//!    claimed by the next node: false), `PublicKeySet::decrypt` of the first
+//!    t+1 shares = the fixture plaintext (a12, a14, a15, a16); the bincode
+//!    layout of `Ciphertext` / `DecryptionShare` that deserialises the
+//!    fixture bytes is reported (version matrix row "ciphertext bytes");
+//!  * bls_ops.json coin: `combine_signatures` of shares 1..=t+1 = the
+//!    fixture signature, `Signature::parity` = the fixture parity (f3);
+//!  * tdec_golden.json threshold_decrypt: hbbft's own `ThresholdDecrypt` of
+//!    node 0 replays every case's `crate_arrival` (shares made by the crate
+//!    on a generated network, the case's bad sender claiming another node's
+//!    share) and must log exactly the fixture's faults per sender
+//!    (MultipleDecryptionShares <-> the repeat flag,
+//!    UnverifiedDecryptionShareSender <-> faulty) and output iff status 0
+//!    (a18).
 //! With `--write` the crate's values are also written to
 //! `<golden dir>/crate_kat.json` (commit it with the Cargo.lock the run wrote:
 //! together they are the version matrix DESIGN.md §3 asks for).  The exit
@@ -26,8 +43,13 @@ use std::sync::Arc;
 
 use hbbft::broadcast::{Broadcast, Message};
 use hbbft::crypto::ff::PrimeField;
-use hbbft::crypto::{Fr, FrRepr, SecretKey};
+use hbbft::crypto::poly::Poly;
+use hbbft::crypto::{Ciphertext, DecryptionShare, Fr, FrRepr, PublicKeySet, SecretKey, SecretKeySet,
+                    SignatureShare};
+use hbbft::threshold_decrypt::{FaultKind as TdFault, Message as TdMessage, ThresholdDecrypt};
 use hbbft::NetworkInfo;
+use serde::de::DeserializeOwned;
+use serde::Serialize;
 use serde_json::{json, Value};
 
 // oracle/synth.py: the seeded payload generator the fixtures were made with
@@ -139,6 +161,187 @@ fn check_frames(dir: &Path, rep: &mut Report) {
     }
 }
 
+/// An Fr from a 32-byte little-endian scalar.
+fn fr(le_hex: &str) -> Fr {
+    let b = hex::decode(le_hex).expect("scalar hex");
+    let mut limbs = [0u64; 4];
+    for (i, l) in limbs.iter_mut().enumerate() {
+        *l = u64::from_le_bytes(b[8 * i..8 * i + 8].try_into().unwrap());
+    }
+    Fr::from_repr(FrRepr(limbs)).expect("scalar < r")
+}
+
+/// Deserialises `T` from the first bincode layout among `forms` that both
+/// parses and re-serialises to the same bytes; returns the value and the
+/// layout's index (point tuples vs length-prefixed byte strings differ
+/// between threshold_crypto versions).
+fn de_any<T: DeserializeOwned + Serialize>(forms: &[Vec<u8>]) -> Option<(T, usize)> {
+    forms.iter().enumerate().find_map(|(i, f)| {
+        let v: T = bincode::deserialize(f).ok()?;
+        if bincode::serialize(&v).ok()? == *f { Some((v, i)) } else { None }
+    })
+}
+
+fn len_prefixed(b: &[u8]) -> Vec<u8> {
+    let mut v = (b.len() as u64).to_le_bytes().to_vec();
+    v.extend_from_slice(b);
+    v
+}
+
+/// The two candidate bincode layouts of a compressed point.
+fn point_forms(b: &[u8]) -> Vec<Vec<u8>> {
+    vec![b.to_vec(), len_prefixed(b)]
+}
+
+/// `Ciphertext(U, V, W)` from the fixture's compressed U, V and compressed W.
+fn ciphertext(u: &[u8], v: &[u8], w: &[u8]) -> (Ciphertext, usize) {
+    let forms: Vec<Vec<u8>> = (0..2)
+        .map(|i| {
+            let mut f = point_forms(u)[i].clone();
+            f.extend_from_slice(&len_prefixed(v));
+            f.extend_from_slice(&point_forms(w)[i]);
+            f
+        })
+        .collect();
+    de_any::<Ciphertext>(&forms).expect("no bincode layout of Ciphertext parses the fixture bytes")
+}
+
+fn decryption_share(b: &[u8]) -> DecryptionShare {
+    de_any::<DecryptionShare>(&point_forms(b)).expect("DecryptionShare layout").0
+}
+
+fn bits(b: bool) -> Vec<u8> {
+    vec![b as u8]
+}
+
+fn check_tdec(dir: &Path, rep: &mut Report) {
+    let g = load(dir, "tdec_golden.json");
+    let sc = &g["scenario"];
+    let t = sc["t"].as_u64().unwrap() as usize;
+    let poly = Poly::from(sc["poly"].as_array().unwrap().iter().map(|c| fr(hex_str(c))).collect::<Vec<Fr>>());
+    let sks = SecretKeySet::from(poly);
+    let pks: PublicKeySet = sks.public_keys();
+    assert_eq!(pks.threshold(), t, "poly degree");
+    for (i, p) in sc["pk_shares"].as_array().unwrap().iter().enumerate() {
+        rep.check(format!("tdec pk_share {}", i), &pks.public_key_share(i).to_bytes(), hex_str(p));
+    }
+    for (k, c) in sc["cts"].as_array().unwrap().iter().enumerate() {
+        let (ct, layout) = ciphertext(&hex::decode(hex_str(&c["U"])).unwrap(), &hex::decode(hex_str(&c["V"])).unwrap(),
+                                      &hex::decode(hex_str(&c["W"])).unwrap());
+        rep.values.insert(format!("tdec ct {} bincode layout", k),
+                          (if layout == 0 { "point tuples" } else { "length-prefixed points" }).to_string());
+        rep.check(format!("tdec ct {} verify", k), &bits(ct.verify()), "01");
+        let shares: Vec<DecryptionShare> = c["shares"].as_array().unwrap().iter()
+            .map(|x| decryption_share(&hex::decode(hex_str(x)).unwrap())).collect();
+        let n = shares.len();
+        for (i, sh) in shares.iter().enumerate() {
+            rep.check(format!("tdec ct {} share {} verify", k, i),
+                      &bits(pks.public_key_share(i).verify_decryption_share(sh, &ct)), "01");
+            // the same bytes claimed by the next node
+            rep.check(format!("tdec ct {} share {} as node {} verify", k, i, (i + 1) % n),
+                      &bits(pks.public_key_share((i + 1) % n).verify_decryption_share(sh, &ct)), "00");
+            // and the crate's own share of node i is the fixture's
+            let own = sks.secret_key_share(i).decrypt_share_no_verify(&ct);
+            rep.check(format!("tdec ct {} share {} bytes", k, i), &bincode::serialize(&own).unwrap()
+                          [bincode::serialize(&own).unwrap().len() - 48..], hex_str(&c["shares"][i]));
+        }
+        let pt = pks.decrypt((0..=t).map(|i| (i, &shares[i])), &ct).expect("PublicKeySet::decrypt");
+        rep.check(format!("tdec ct {} decrypt", k), &pt, hex_str(&c["plaintext"]));
+    }
+}
+
+fn check_coin(dir: &Path, rep: &mut Report) {
+    let g = load(dir, "bls_ops.json");
+    let c = &g["coin"];
+    let t = c["t"].as_u64().unwrap() as usize;
+    // the coin uses the tdec scenario's key set (tests/golden/make_golden_bls.py)
+    let sc = load(dir, "tdec_golden.json");
+    let poly = Poly::from(sc["scenario"]["poly"].as_array().unwrap().iter().map(|x| fr(hex_str(x)))
+                              .collect::<Vec<Fr>>());
+    let pks = SecretKeySet::from(poly).public_keys();
+    rep.check("coin pk".to_string(), &pks.public_key().to_bytes(), hex_str(&c["pk"]));
+    for (j, coin) in c["coins"].as_array().unwrap().iter().enumerate() {
+        let shares: Vec<SignatureShare> = coin["shares"].as_array().unwrap().iter()
+            .map(|x| de_any::<SignatureShare>(&point_forms(&hex::decode(hex_str(x)).unwrap()))
+                 .expect("SignatureShare layout").0)
+            .collect();
+        let doc = hex::decode(hex_str(&coin["doc"])).unwrap();
+        for (i, sh) in shares.iter().enumerate() {
+            rep.check(format!("coin {} share {} verify", j, i), &bits(pks.public_key_share(i).verify(sh, &doc)), "01");
+        }
+        let sig = pks.combine_signatures((1..=t + 1).map(|i| (i, &shares[i]))).expect("combine_signatures");
+        rep.check(format!("coin {} sig", j), &sig.to_bytes(), hex_str(&coin["sig"]));
+        let want = if coin["parity"].as_bool().unwrap() { "01" } else { "00" };
+        rep.check(format!("coin {} parity", j), &bits(sig.parity()), want);
+    }
+}
+
+fn check_threshold_decrypt(dir: &Path, rep: &mut Report) {
+    let g = load(dir, "tdec_golden.json");
+    let sc = &g["scenario"];
+    let a = &g["threshold_decrypt"];
+    let n = sc["pk_shares"].as_array().unwrap().len();
+    let our = a["our_node"].as_u64().unwrap() as usize;
+    let rf = a["outcome_codes"]["repeat_flag"].as_u64().unwrap() as u8;
+    let faulty = a["outcome_codes"]["faulty"].as_u64().unwrap() as u8;
+    let mut rng = rand::thread_rng();
+    let infos: BTreeMap<usize, NetworkInfo<usize>> =
+        NetworkInfo::generate_map(0..n, &mut rng).expect("NetworkInfo::generate_map");
+    for (ci, c) in a["cases"].as_array().unwrap().iter().enumerate() {
+        let k = c["ct"].as_u64().unwrap() as usize;
+        let msg = hex::decode(hex_str(&sc["cts"][k]["plaintext"])).unwrap();
+        let ct = infos[&our].public_key_set().public_key().encrypt(&msg);
+        let mut shares: Vec<DecryptionShare> = (0..n)
+            .map(|i| infos[&i].secret_key_share().expect("validator").decrypt_share_no_verify(&ct))
+            .collect();
+        let bad = c["bad_sender"].as_u64().unwrap() as usize;
+        shares[bad] = shares[(bad + 1) % n].clone();
+        let mut td = ThresholdDecrypt::new(Arc::new(infos[&our].clone()));
+        let mut faults: BTreeMap<usize, Vec<String>> = BTreeMap::new();
+        let mut output: Option<Vec<u8>> = None;
+        let mut absorb = |step: hbbft::threshold_decrypt::Step<usize>| {
+            for f in step.fault_log.0.iter() {
+                faults.entry(f.node_id).or_default().push(format!("{:?}", f.kind));
+            }
+            if let Some(o) = step.output.into_iter().next() {
+                output = Some(o);
+            }
+        };
+        let arr = c["crate_arrival"].as_array().unwrap();
+        let start = |td: &mut ThresholdDecrypt<usize>| {
+            td.set_ciphertext(ct.clone()).expect("set_ciphertext");
+            td.start_decryption().expect("start_decryption")
+        };
+        if !arr.iter().any(|x| x.is_string()) {
+            absorb(start(&mut td));
+        }
+        for x in arr {
+            if x.is_string() {
+                absorb(start(&mut td));
+            } else {
+                let s = x.as_u64().unwrap() as usize;
+                absorb(td.handle_message(&s, TdMessage(shares[s].clone())).expect("handle_message"));
+            }
+        }
+        let oc = c["outcome"].as_array().unwrap();
+        for (s, o) in oc.iter().enumerate() {
+            let o = o.as_u64().unwrap() as u8;
+            let got = faults.get(&s).cloned().unwrap_or_default();
+            let want_repeat = o & rf != 0;
+            let want_unverified = o & 3 == faulty;
+            let has = |kind: TdFault| got.iter().any(|g| *g == format!("{:?}", kind));
+            let ok = has(TdFault::MultipleDecryptionShares) == want_repeat
+                && has(TdFault::UnverifiedDecryptionShareSender) == want_unverified;
+            rep.check(format!("a18 case {} sender {} faults", ci, s), &bits(ok), "01");
+        }
+        let status = c["status"].as_i64().unwrap();
+        rep.check(format!("a18 case {} output", ci), &bits(output.is_some()), if status == 0 { "01" } else { "00" });
+        if let Some(o) = output {
+            rep.check(format!("a18 case {} plaintext", ci), &o, &hex::encode(&msg));
+        }
+    }
+}
+
 fn check_hash_g2(dir: &Path, rep: &mut Report) {
     let g = load(dir, "tdec_golden.json");
     let one = secret_key(&format!("01{}", "00".repeat(31)));
@@ -157,6 +360,9 @@ fn main() {
     check_wire(&dir, &mut rep);
     check_frames(&dir, &mut rep);
     check_hash_g2(&dir, &mut rep);
+    check_tdec(&dir, &mut rep);
+    check_coin(&dir, &mut rep);
+    check_threshold_decrypt(&dir, &mut rep);
     println!("kat-gen: {} comparisons, {} mismatches", rep.checked, rep.failed);
     if write {
         let out = json!({"generator": "rust/kat-gen", "values": rep.values});

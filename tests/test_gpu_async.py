@@ -237,7 +237,7 @@ def test_sig_combine_rejects_wrapping_threshold():
     out = np.zeros(96, np.uint8)
     par = np.zeros(1, np.uint8)
     st = np.zeros(1, np.int32)
-    for t in (32, 0xFFFFFFFF):
+    for t in (64, 0xFFFFFFFF):
         assert _lib.lib().hbg_sig_combine(ctx.h, t, 1, _lib.ptr(sh), _lib.ptr(ix), _lib.ptr(out), _lib.ptr(par),
                                           _lib.ptr(st), 0) == _lib.HBG_E_ARG
 

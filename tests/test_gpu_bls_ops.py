@@ -148,7 +148,7 @@ def test_coin_sign_verify_combine_matches_fixture():
         assert th.PublicKey(bytes.fromhex(c["pk"])).verify(bytes.fromhex(coin["sig"]), doc)
 
 
-@pytest.mark.parametrize("t", [0, 3, 21, 31])
+@pytest.mark.parametrize("t", [0, 3, 21, 31, 42, 63])
 def test_coin_combine_arbitrary_points(t):
     """hbg_sig_combine over arbitrary G2 points (interpolation does not need
     valid shares), odd coin count, identity shares, sparse shuffled indices,

@@ -21,7 +21,7 @@ timeout -k 10 900 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OU
 cut -c1-1500 "$OUT/bench.json"
 if [ -z "${NO_PROF:-}" ]; then
   echo "== rocprofv3 kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python bench.py --steps 5 --warmup 1 --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
       || { tail -30 "$OUT/prof.err"; exit 6; }
 fi
