@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -167,12 +168,23 @@ class Context:
 
 
 _default: Context | None = None
+_default_stream: int | None = None
 
 
 def default_context() -> Context:
-    global _default
+    """The process-wide context of the convenience wrappers.  Once torch has
+    initialised the GPU it follows torch's current stream (hbg_set_stream
+    orders the switch), so device tensors torch just wrote are ready for it
+    and its results are ready for torch — no extra synchronisation."""
+    global _default, _default_stream
     if _default is None:
         _default = Context()
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        h = torch.cuda.current_stream().cuda_stream
+        if h != _default_stream:
+            _default.set_stream(h)
+            _default_stream = h
     return _default
 
 

@@ -47,9 +47,11 @@ struct hbg_ctx {
     // rounds); 2 batched + pk tables always (and, for signature shares, no speculative 16-group round);
     // 3 batched at every size.  pk fixed-base tables when each key verifies >= kPkTableMinUses shares.
     int tdec_batched = 1;
-    // hbg_rbc_encode_merkle schedule (hbg_test_set_rbc_fused): 0 rs_encode_const + merkle_build, 1 fused
-    int rbc_fused = 0;
+    // hbg_rbc_encode_merkle schedule (hbg_test_set_rbc_fused): 0 rs_encode_const + merkle_build, 1 the
+    // fused rbc_encode_merkle, -1 (default) fused where it measured faster: (D, Q) = (22, 42), N = 64
+    int rbc_fused = -1;
     int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
+    hipEvent_t switch_ev = nullptr;  // hbg_set_stream: orders the new stream after the old one
     std::mutex mu;
 };
 
@@ -305,22 +307,33 @@ void hbg_free(hbg_ctx* c) {
     for (auto& kv : c->matrices) (void)hipFree(kv.second);
     for (auto& kv : c->enc_plans) (void)hipFree(kv.second);
     (void)hipFree(c->d_err);
+    if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
     (void)hipStreamDestroy(c->own);
     delete c;
+}
+
+// Work enqueued on the old stream completes before anything enqueued on the
+// new one (event record + stream wait: no host synchronisation).
+static int switch_stream(hbg_ctx* c, hipStream_t s) {
+    if (s == c->stream) return HBG_OK;
+    HBG_TRY(hipSetDevice(c->device));
+    if (!c->switch_ev) HBG_TRY(hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming));
+    HBG_TRY(hipEventRecord(c->switch_ev, c->stream));
+    HBG_TRY(hipStreamWaitEvent(s, c->switch_ev, 0));
+    c->stream = s;
+    return HBG_OK;
 }
 
 int hbg_set_stream(hbg_ctx* c, void* s) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    c->stream = (hipStream_t)s;
-    return HBG_OK;
+    return switch_stream(c, (hipStream_t)s);
 }
 
 int hbg_reset_stream(hbg_ctx* c) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    c->stream = c->own;
-    return HBG_OK;
+    return switch_stream(c, c->own);
 }
 
 int hbg_sync(hbg_ctx* c) {
@@ -455,7 +468,8 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
     auto run = [&](const uint8_t* dpay, uint64_t dps, const uint64_t* dplen, uint8_t* dsh, uint64_t S,
                    uint8_t* dlev) -> int {
         HBG_TRY(launch_rbc_check_plen(n, dplen, dps, D, L, c->d_err, c->stream));
-        if (c->rbc_fused && Q && const_encoder_fits(D, Q, S, dps, true)) {  // one launch: encode + leaves + tree
+        const bool fused = c->rbc_fused == 1 || (c->rbc_fused < 0 && D == 22 && Q == 42);
+        if (fused && Q && const_encoder_fits(D, Q, S, dps, true)) {  // one launch: encode + leaves + tree
             HBG_TRY(launch_rbc_encode_merkle(D, Q, dsh, S, L, n, dpay, dps, dplen, dlev, c->stream));
             return HBG_OK;
         }
@@ -1215,7 +1229,7 @@ int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
 int hbg_test_set_rbc_fused(hbg_ctx* c, int on) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    if (on < 0 || on > 1) return HBG_E_ARG;
+    if (on < -1 || on > 1) return HBG_E_ARG;
     c->rbc_fused = on;
     return HBG_OK;
 }

@@ -101,7 +101,7 @@ __device__ __forceinline__ u32x2_a4 payload_window(const EncodeRows& r, uint32_t
     return u32x2_a4{v[0], v[1]};
 }
 
-template <int D, int Q, int MODE>
+template <int D, int Q, int MODE, bool RING_DATA = false>
 struct EncodeCtx {
     const EncodeRows& r;
     u32x2_a4 buf[kPrefetch];
@@ -134,6 +134,7 @@ struct EncodeCtx {
         }
         if constexpr (MODE != 0)
             __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), 0);
+        if constexpr (RING_DATA) r.ring[(J - D) * (int)r.rdw] = w;  // data rows sit below the parity rows
         return w;
     }
 
@@ -165,9 +166,9 @@ struct EncodeCtx {
 // Column p0 + t of every row: data words (MODE 1/2: from the payload, stored
 // to the data rows) and the Q parity words.
 // RING: the parity words also go to the fused kernel's LDS ring (r.ring).
-template <int D, int Q, int MODE, bool RING = false>
+template <int D, int Q, int MODE, bool RING = false, bool RING_DATA = false>
 __device__ __forceinline__ void encode_word(const EncodeRows& r) {
-    EncodeCtx<D, Q, MODE> cx{r, {}};
+    EncodeCtx<D, Q, MODE, RING_DATA> cx{r, {}};
     uint32_t acc[Q];
 #pragma unroll
     for (int k = 0; k < Q; ++k) acc[k] = 0u;
@@ -546,6 +547,14 @@ __host__ __device__ constexpr uint32_t fused_ring_bytes(uint32_t pass_bytes) {
     return r;
 }
 
+// Where the absorb of a data row reads its block: 0 the shard row just stored
+// (sc1 loads), 1 the payload itself for blocks inside it (per-lane unaligned:
+// 18 loads + v_alignbyte), 2 the LDS ring (all N rows in the ring).
+#ifndef HBG_FUSED_DATA_SRC
+#define HBG_FUSED_DATA_SRC 0
+#endif
+constexpr int kFusedDataSrc = HBG_FUSED_DATA_SRC;
+
 template <int D, int Q>
 struct FusedShape {
     static constexpr uint32_t N = D + Q;
@@ -554,7 +563,8 @@ struct FusedShape {
     static constexpr uint32_t IPB = BLK / LPI;
     static constexpr uint32_t NODES = merkle_nodes(N);
     static constexpr uint32_t R = fused_ring_bytes(4 * LPI);  // ring bytes per parity row
-    static constexpr uint32_t RING = IPB * Q * R;
+    static constexpr uint32_t RROWS = kFusedDataSrc == 2 ? D + Q : Q;  // rows kept in the ring
+    static constexpr uint32_t RING = IPB * RROWS * R;
     static constexpr uint32_t TREE = IPB * NODES * 32;
     static constexpr uint32_t LDS = RING > TREE ? RING : TREE;
     static constexpr int WPE = 2;  // waves per SIMD the register budget is sized for
@@ -581,12 +591,13 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     // is left unwritten (no shards, no levels)
     const bool live = inst < n && payload_fits(P, pstride, D, L);
     uint8_t* base = shards + inst * (uint64_t)N * S;
-    uint32_t* ring = ring_all + sub * (Q * R / 4);  // this instance's parity rows
+    constexpr uint32_t RD = kFusedDataSrc == 2 ? (uint32_t)D : 0u;  // ring row of parity row 0
+    uint32_t* ring = ring_all + sub * (F::RROWS * R / 4) + RD * (R / 4);  // this instance's parity row 0
     uint32_t* tree = tree_all + sub * NODES * 8;
     const uint64_t cols = (L + 3) / 4;
     const uint32_t passes = (uint32_t)((cols + LPI - 1) / LPI);
     const bool row_lane = live && t < N;
-    const bool ring_lane = row_lane && t >= (uint32_t)D;
+    const bool ring_lane = row_lane && (kFusedDataSrc == 2 || t >= (uint32_t)D);
     // buffer resources over the workgroup's first instance (uniform); a lane's
     // instance and column / row are VGPR offsets (host: IPB * N * S and
     // IPB * pstride < 2^31)
@@ -596,7 +607,8 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     r.rdw = R / 4;
     const uint32_t vrow = (uint32_t)((sub * N + t) * S);  // absorb: this lane's row
     // absorb (parity lanes): row t - D of the ring, as 8-byte words
-    const uint64_t* rrow = reinterpret_cast<const uint64_t*>(ring + (ring_lane ? t - D : 0) * (R / 4));
+    const uint64_t* rrow =
+        reinterpret_cast<const uint64_t*>(ring + (ring_lane ? (int)t - D : 0) * (int)(R / 4));
     u64p a[25];
     keccak_zero(a);
     uint32_t done = 0;  // 136-byte blocks absorbed (the same count for every row)
@@ -612,6 +624,24 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             const uint32_t rp = (136u * done) % R / 8;
 #pragma unroll
             for (int i = 0; i < 17; ++i) w[i] = rrow[rp + i];
+        } else if (kFusedDataSrc == 1 && (uint64_t)t * L + 136ull * done >= 4 &&
+                   (uint64_t)t * L + 136ull * done + 140 <= P + 4) {
+            // data row t's block is payload bytes [o, o + 136), o = t L + 136 done - 4:
+            // 35 dwords from the dword below o, then a per-lane byte shift
+            const uint64_t o = (uint64_t)t * L + 136ull * done - 4;
+            const uint32_t a = (uint32_t)(o & ~3ull), sh8 = (uint32_t)(o & 3);
+            uint32_t d[35];
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.py, (uint32_t)(sub * pstride) + a + 8 * i, 0, 0);
+                d[2 * i] = v[0];
+                d[2 * i + 1] = v[1];
+            }
+            d[34] = __builtin_amdgcn_raw_buffer_load_b32(r.py, (uint32_t)(sub * pstride) + a + 136, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 17; ++i)
+                w[i] = (uint64_t)__builtin_amdgcn_alignbyte(d[2 * i + 1], d[2 * i], sh8) |
+                       ((uint64_t)__builtin_amdgcn_alignbyte(d[2 * i + 2], d[2 * i + 1], sh8) << 32);
         } else {
 #pragma unroll
             for (int i = 0; i < 17; ++i) {
@@ -631,12 +661,13 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         if (wpos >= R) wpos -= R;
         r.ring = ring + wpos / 4;
         if (live) {
+            constexpr bool RDATA = kFusedDataSrc == 2;
             if (have_pre) {
-                encode_word<D, Q, 3, true>(r);
+                encode_word<D, Q, 3, true, RDATA>(r);
             } else if (interior(ps)) {
-                encode_word<D, Q, 2, true>(r);
+                encode_word<D, Q, 2, true, RDATA>(r);
             } else if (4 * (uint64_t)p < L) {
-                encode_word<D, Q, 1, true>(r);
+                encode_word<D, Q, 1, true, RDATA>(r);
             }
         }
         // the pass's stores are complete in L2 (data rows) and in LDS (parity

@@ -86,7 +86,9 @@ void hbg_free(hbg_ctx *ctx);
 /* Enqueue on an external hipStream_t from now on (e.g.
  * torch.cuda.current_stream().cuda_stream); the handle is used verbatim, so
  * NULL selects the HIP null stream.  hbg_reset_stream() returns to the
- * context's own non-blocking stream. */
+ * context's own non-blocking stream.  A switch is ordered: work enqueued on
+ * the old stream completes before work enqueued on the new one (an event,
+ * no host synchronisation). */
 int hbg_set_stream(hbg_ctx *ctx, void *hip_stream);
 int hbg_reset_stream(hbg_ctx *ctx);
 int hbg_sync(hbg_ctx *ctx);

@@ -20,10 +20,11 @@ extern "C" {
  * check per share.  All return identical bits. */
 int hbg_test_set_tdec_batched(hbg_ctx *ctx, int on);
 /* Choose the schedule of hbg_rbc_encode_merkle for the (D, Q) with a
- * compile-time coding matrix: 0 (the default) rs_encode_const then
- * merkle_build (two launches), 1 the single-launch rbc_encode_merkle kernel
- * (encode pass + SHA3 leaves + tree).  Both write identical shards and
- * levels; the fused one is the slower on MI355X. */
+ * compile-time coding matrix: 0 rs_encode_const then merkle_build (two
+ * launches), 1 the single-launch rbc_encode_merkle kernel (encode pass +
+ * LDS transpose + SHA3 leaves + tree), -1 (the default) the fused kernel
+ * where it measured faster on MI355X — (D, Q) = (22, 42), N = 64 — and two
+ * launches elsewhere.  Both write identical shards and levels. */
 int hbg_test_set_rbc_fused(hbg_ctx *ctx, int on);
 int hbg_test_bls(hbg_ctx *ctx, int op, uint32_t n, const uint32_t *in, uint32_t in_words, uint32_t *out,
                  uint32_t out_words);

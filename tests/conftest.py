@@ -27,3 +27,18 @@ def ctx():
     from hydrabadger_amd import _lib
     c = _lib.default_context()
     yield c
+
+
+@pytest.fixture(autouse=True)
+def _default_context_left_clean(request):
+    """A GPU test must not leave a sticky device error (or a pending HIP
+    error) on the shared default context: the next test's synchronising
+    call would report it.  Checked after every gpu-marked test that used it."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    from hydrabadger_amd import _lib
+    if _lib._default is None:
+        return
+    rc = _lib.lib().hbg_sync(_lib._default.h)
+    assert rc == _lib.HBG_OK, f"{request.node.nodeid} left device error {rc} on the default context"

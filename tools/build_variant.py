@@ -6,6 +6,10 @@ HBG_LIB_PATH.
 
     python tools/build_variant.py fpcount -DHBG_FP_COUNT
     python tools/build_variant.py debug -DHBG_DEBUG_CHECKS
+    HBG_VARIANT_ONLY=rbc_kernels.hip python tools/build_variant.py ring2 -DHBG_FUSED_DATA_SRC=2
+
+HBG_VARIANT_ONLY=<file.hip>: recompile only that source with the flags and
+link it with the product objects of the others (hydrabadger_amd/build/).
 """
 from __future__ import annotations
 
@@ -26,7 +30,11 @@ def build(name: str, defines: list) -> str:
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(hb.CSRC, "*.hip")))
 
+    only = os.environ.get("HBG_VARIANT_ONLY")
+
     def one(src):
+        if only and os.path.basename(src) != only:
+            return os.path.join(hb.OBJ, os.path.basename(src) + ".o")
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
         r = subprocess.run([hb.HIPCC, *hb.CFLAGS, *defines, "-c", src, "-o", obj], capture_output=True, text=True)
         if r.returncode:

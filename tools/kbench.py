@@ -65,15 +65,17 @@ def main():
         if "merkle" in whats:
             res["merkle_ms"] = t(lambda: bc.merkle_build_batch(N, L, shards, levels, ctx=ctx, device=True,
                                                                 asynchronous=True))
-        if "encode" in whats:
+        if "encode" in whats:  # the two-launch schedule (rs_encode_const -> merkle_build)
+            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, 0))
             res["encode_merkle_ms"] = t(lambda: bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels, ctx=ctx,
                                                                           device=True, asynchronous=True))
+            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, -1))
         if "fused" in whats:  # the single-launch schedule (hbg_test_set_rbc_fused)
             _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, 1))
             res["encode_merkle_fused_ms"] = t(lambda: bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels,
                                                                                 ctx=ctx, device=True,
                                                                                 asynchronous=True))
-            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, 0))
+            _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, -1))
         if "rs" in whats:
             def rs():
                 _lib.check(_lib.lib().hbg_rs_encode(ctx.h, D, Q, L, shards.data_ptr(), S, B,
