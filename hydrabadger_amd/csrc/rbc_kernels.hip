@@ -548,10 +548,21 @@ __host__ __device__ constexpr uint32_t fused_ring_bytes(uint32_t pass_bytes) {
 }
 
 // Where the absorb of a data row reads its block: 0 the shard row just stored
-// (sc1 loads), 1 the payload itself for blocks inside it (per-lane unaligned:
-// 18 loads + v_alignbyte), 2 the LDS ring (all N rows in the ring).
+// (sc1 loads), 1 (default) the payload itself for blocks inside it (per-lane
+// unaligned: 18 loads + v_alignbyte; L2-resident, the encoder loaded the same
+// lines one pass earlier), 2 the LDS ring (all N rows in the ring).  Measured
+// at 8,192 x 1 MiB (profiles/r03i): 27.8 / 26.6 / 33.5 ms — the ring of all
+// rows halves the waves a CU holds (26 KB of LDS per wave).
 #ifndef HBG_FUSED_DATA_SRC
-#define HBG_FUSED_DATA_SRC 0
+#define HBG_FUSED_DATA_SRC 1
+#endif
+// waves per SIMD the fused kernel's register budget is sized for, and
+// whether the next pass's payload windows are prefetched into registers
+#ifndef HBG_FUSED_WPE
+#define HBG_FUSED_WPE 2
+#endif
+#ifndef HBG_FUSED_PREFETCH
+#define HBG_FUSED_PREFETCH 1
 #endif
 constexpr int kFusedDataSrc = HBG_FUSED_DATA_SRC;
 
@@ -567,7 +578,7 @@ struct FusedShape {
     static constexpr uint32_t RING = IPB * RROWS * R;
     static constexpr uint32_t TREE = IPB * NODES * 32;
     static constexpr uint32_t LDS = RING > TREE ? RING : TREE;
-    static constexpr int WPE = 2;  // waves per SIMD the register budget is sized for
+    static constexpr int WPE = HBG_FUSED_WPE;  // waves per SIMD the register budget is sized for
 };
 
 template <int D, int Q>
@@ -676,7 +687,7 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         __syncthreads();
         const uint64_t written = 4ull * LPI * (ps + 1);
         const uint64_t avail = written < L ? written : L;
-        const bool next_pre = live && ps + 1 < passes && interior(ps + 1);
+        const bool next_pre = HBG_FUSED_PREFETCH && live && ps + 1 < passes && interior(ps + 1);
         have_pre = false;
         auto prefetch = [&]() {
             if (next_pre && !have_pre) {
