@@ -159,6 +159,13 @@ def cpu_baseline(n_sample: int):
 # nominal clock on 1,024 SIMDs: 35.4 T lane-MADs/s.
 MADS_PER_FP_MUL = 288
 MAD_PEAK = 256 * 4 * 64 / 4.44 * 2.4e9
+# The issue bound of a whole Fp multiplication: 288 v_mad_u64_u32 + 288
+# v_addc_co_u32_e64 (both half rate on gfx950: 4.34 / 4.33 cycles per
+# wave-instruction per SIMD at 8 waves/SIMD, profiles/r03/ubench5_fp_mul_issue.txt)
+# + ~100 full-rate VALU (2.25): 2,720 cycles per wave-multiplication, so
+# 1,024 SIMDs x 64 lanes x 2.4 GHz / 2,720 = 57.8 G Fp mul/s chip-wide.
+FP_MUL_ISSUE_CYCLES = 288 * 4.34 + 288 * 4.33 + 100 * 2.25
+FP_MUL_PEAK = 256 * 4 * 64 * 2.4e9 / FP_MUL_ISSUE_CYCLES
 
 
 def fp_count_profile(n_nodes: int, t: int, bad_rate: float) -> dict:
@@ -357,6 +364,12 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             "bound": "valu", "unit": "T v_mad_u64_u32/s",
             "achieved": achieved / 1e12, "peak": MAD_PEAK / 1e12, "frac": achieved / MAD_PEAK,
             "fp_mul_per_share": per_share, "mads_per_fp_mul": MADS_PER_FP_MUL,
+            "fp_mul_issue_bound": {
+                "achieved_G_fp_mul_per_s": per_share * n / (ms * 1e-3) / 1e9,
+                "peak_G_fp_mul_per_s": FP_MUL_PEAK / 1e9,
+                "frac": per_share * n / (ms * 1e-3) / FP_MUL_PEAK,
+                "note": "peak = whole-multiplication issue rate (288 mad + 288 addc, both half rate, + ~100 "
+                        "full-rate VALU) measured on gfx950 (profiles/r03/ubench5_fp_mul_issue.txt)"},
             "verify_only": {"achieved": achieved_v / 1e12, "frac": achieved_v / MAD_PEAK,
                             "fp_mul_per_share": per_share_v},
             "traffic": None, "count_source": prof["path"] + " (" + prof.get("source", "") + ")",
