@@ -182,3 +182,26 @@ def test_epoch_small_networks_oracle_engine(N, spec):
     spec = {k: {x % N for x in v} for k, v in spec.items()}
     res = hbe.HoneyBadgerEpoch(N, 17, OracleEngine(), seed=4).run(epoch=3, faults=_faults(spec, hbe))
     compare(res, oep.run_epoch(N, 17, seed=4, epoch=3, faults=_faults(spec, oep)), 17)
+
+
+@pytest.mark.gpu
+def test_epoch_device_configs4_size():
+    """BASELINE.json configs[4] at full size on one GPU: a 128-node epoch (RS
+    44+84, t = 42) with 1 MiB contributions — every contribution delivered,
+    accepted and decrypted to its bytes, t+1 shares held per ciphertext
+    (size-independent properties; no oracle epoch at this size)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import network
+    eng = network.DeviceEngine(torch.device("cuda:0"))
+    try:
+        N, P = 128, 1 << 20
+        res = hbe.HoneyBadgerEpoch(N, P, eng, seed=7).run(epoch=3)
+        assert bool(res.delivered.all()) and res.accepted == list(range(N))
+        assert _np(res.ct_status).tolist() == [0] * N
+        want = eng.synth(hbe.TAG_CONTRIB, hbe.instance_id(3, 0), N, P)
+        assert torch.equal(res.plaintexts, want)
+        oc = _np(res.share_outcome)
+        assert ((oc == 1).sum(1) == 43).all() and ((oc == 3).sum(1) == N - 43).all()
+    finally:
+        eng.ctx.close()
