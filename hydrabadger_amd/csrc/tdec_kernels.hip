@@ -251,6 +251,141 @@ __global__ __launch_bounds__(64) void tdec_v_digest(uint64_t n, const uint8_t* _
     if (len > 64) sha3_long(V + o, len, dig + 32 * k);
 }
 
+// Low-latency SHA3-256 of one long message per WAVE (few items, MiB-sized V:
+// the configs[4] epoch hashes 128 contributions of 1 MiB, where one lane per
+// item leaves the GPU idle and each sponge is 7,710 dependent permutations).
+// Lane l < 25 holds state word l = x + 5y as (lo, hi); a round is
+//   theta  column parity from the 4 other lanes of the column, then C[x-1]
+//          and C[x+1] from the neighbour lanes (ds_bpermute gathers),
+//   rho    each lane rotates its own word by its own offset (64-bit shifts),
+//   pi+chi each lane gathers the rotated words of its pi source and of the
+//          sources of (x+1, y), (x+2, y) and applies chi,
+//   iota   lane 0 only (a lane mask ANDed with the round constant),
+// ~35 VALU + 18 cross-lane gathers per round instead of the 190-instruction
+// round of one lane.  Blocks are absorbed by lanes 0..16 (8 message bytes
+// each, the next block's dwords prefetched during the current permutation).
+#ifndef HBG_VDIG_THETA1
+#define HBG_VDIG_THETA1 0
+#endif
+constexpr uint8_t kRhoOff[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39,
+                                 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+
+__global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8_t* __restrict__ V,
+                                                         const uint64_t* __restrict__ off,
+                                                         uint8_t* __restrict__ dig) {
+    const uint64_t k = blockIdx.x;
+    if (k >= n) return;
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    if (len <= 64) return;  // hashed inline by hash_g1_g2_msg's caller
+    const uint32_t l = threadIdx.x, ls = l < 25 ? l : l % 25;
+    const uint32_t x = ls % 5, y = ls / 5;
+    uint32_t col[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j] = x + 5 * ((y + 1 + j) % 5);
+    const uint32_t cm1 = (x + 4) % 5 + 5 * y, cp1 = (x + 1) % 5 + 5 * y;
+    uint32_t cmcol[5], cpcol[5];  // the lanes of columns x-1 and x+1
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        cmcol[j] = (x + 4) % 5 + 5 * j;
+        cpcol[j] = (x + 1) % 5 + 5 * j;
+    }
+    // B[X][Y] = rho(A[x][y]) with X = y, Y = 2x + 3y: the source of (X, Y) is
+    // x = 3 (Y - 3X) mod 5, y = X
+    auto pisrc = [](uint32_t X, uint32_t Y) { return (3 * (Y + 15 - 3 * X)) % 5 + 5 * X; };
+    const uint32_t s0 = pisrc(x, y), s1 = pisrc((x + 1) % 5, y), s2 = pisrc((x + 2) % 5, y);
+    const uint32_t r = kRhoOff[ls], rr = (64 - r) & 63;
+    const uint32_t lane0 = l == 0 ? 0xFFFFFFFFu : 0u;
+    uint32_t lo = 0, hi = 0;
+    auto permute = [&]() {
+        for (int rnd = 0; rnd < 24; ++rnd) {
+#if HBG_VDIG_THETA1
+            // C[x-1] and C[x+1] straight from the 10 lanes of the two columns:
+            // one gather stage instead of two
+            uint32_t mlo = 0, mhi = 0, plo = 0, phi = 0;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                mlo ^= lane_get(lo, cmcol[j]);
+                mhi ^= lane_get(hi, cmcol[j]);
+                plo ^= lane_get(lo, cpcol[j]);
+                phi ^= lane_get(hi, cpcol[j]);
+            }
+#else
+            uint32_t clo = lo, chi = hi;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                clo ^= lane_get(lo, col[j]);
+                chi ^= lane_get(hi, col[j]);
+            }
+            const uint32_t mlo = lane_get(clo, cm1), mhi = lane_get(chi, cm1);
+            const uint32_t plo = lane_get(clo, cp1), phi = lane_get(chi, cp1);
+#endif
+            lo = __builtin_amdgcn_bitop3_b32(lo, mlo, __builtin_amdgcn_alignbit(plo, phi, 31), 0x96);
+            hi = __builtin_amdgcn_bitop3_b32(hi, mhi, __builtin_amdgcn_alignbit(phi, plo, 31), 0x96);
+            uint64_t w = ((uint64_t)hi << 32) | lo;
+            w = (w << r) | (w >> rr);
+            const uint32_t wlo = (uint32_t)w, whi = (uint32_t)(w >> 32);
+            const uint32_t b0l = lane_get(wlo, s0), b0h = lane_get(whi, s0);
+            const uint32_t b1l = lane_get(wlo, s1), b1h = lane_get(whi, s1);
+            const uint32_t b2l = lane_get(wlo, s2), b2h = lane_get(whi, s2);
+            lo = __builtin_amdgcn_bitop3_b32(b0l, b1l, b2l, 0xd2) ^ (lane0 & kKeccakRC[2 * rnd]);
+            hi = __builtin_amdgcn_bitop3_b32(b0h, b1h, b2h, 0xd2) ^ (lane0 & kKeccakRC[2 * rnd + 1]);
+        }
+    };
+    const uint8_t* p = V + o;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+    const bool msg_lane = l < 17;
+    const uint32_t li = msg_lane ? l : 0u;
+    const uint64_t nfull = len / 136;
+    // lane li's 8 bytes of block b: dwords 34 b + 2 li .. + 2 of the aligned view
+    // (the third only when the message is unaligned: the dword holding byte
+    // 136 b + 8 li + 7 is readable because that byte is a message byte)
+    uint32_t d0 = 0, d1 = 0, d2 = 0;
+    auto fetch = [&](uint64_t b) {
+        const uint32_t* qb = q + 34 * b + 2 * li;
+        d0 = qb[0];
+        d1 = qb[1];
+        d2 = sh ? qb[2] : 0u;
+    };
+    if (nfull) fetch(0);
+    for (uint64_t b = 0; b < nfull; ++b) {
+        const uint32_t wl = __builtin_amdgcn_alignbyte(d1, d0, sh), wh = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        if (msg_lane) {
+            lo ^= wl;
+            hi ^= wh;
+        }
+        if (b + 1 < nfull) fetch(b + 1);  // in flight during this permutation
+        permute();
+    }
+    // final block: bytes [136 nfull, len) + FIPS-202 padding 0x06 .. 0x80
+    const uint32_t rem = (uint32_t)(len - 136 * nfull);
+    uint32_t wl = 0, wh = 0;
+    if (msg_lane) {
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t pos = 8 * li + i;
+            uint32_t byte = pos < rem ? (uint32_t)p[136 * nfull + pos] : 0u;
+            if (pos == rem) byte ^= 0x06u;
+            if (pos == 135) byte ^= 0x80u;
+            if (i < 4) wl |= byte << (8 * i);
+            else wh |= byte << (8 * (i - 4));
+        }
+        lo ^= wl;
+        hi ^= wh;
+    }
+    permute();
+    if (l < 4) {
+        uint8_t* d = dig + 32 * k + 8 * l;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            d[b] = (uint8_t)(lo >> (8 * b));
+            d[4 + b] = (uint8_t)(hi >> (8 * b));
+        }
+    }
+}
+
 // hash_g1_g2's message m = (|V| > 64 ? SHA3(V) : V) || compress(U); returns
 // |m| (dig: tdec_v_digest's output for this item).
 BD uint32_t hash_g1_g2_msg(const uint8_t* V, uint64_t len, const uint8_t* dig, const uint8_t* u48,
@@ -1988,10 +2123,16 @@ static void count_mark(const char* name, hipStream_t st) {
 #else
 #define HBG_COUNT_MARK(name, st) ((void)0)
 #endif
+// Up to this many items per call SHA3(V) runs one wave per item (latency);
+// beyond it one lane per item (throughput: configs[3]'s 100 k short V).
+constexpr uint64_t kVDigestWaveMax = 8192;
 hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_off, uint8_t* dig, hipStream_t st) {
     HBG_COUNT_MARK("tdec_v_digest", st);
     if (n == 0) return hipSuccess;
-    tdec_v_digest<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(n, V, V_off, dig);
+    if (n <= kVDigestWaveMax)  // few items (the epoch's contributions): one wave per sponge
+        tdec_v_digest_wave<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
+    else
+        tdec_v_digest<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(n, V, V_off, dig);
     return hipGetLastError();
 }
 hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uint8_t* in, const uint64_t* off,
