@@ -52,6 +52,9 @@ struct hbg_ctx {
     int rbc_fused = -1;
     int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
     hipEvent_t switch_ev = nullptr;  // hbg_set_stream: orders the new stream after the old one
+    // a second stream for independent launches inside one call (fork / join by events)
+    hipStream_t aux = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     std::mutex mu;
 };
 
@@ -94,6 +97,7 @@ int scratch(hbg_ctx* c, int i, size_t bytes, void** out) {
     if (b.cap < bytes) {
         if (b.p) {
             HBG_TRY(hipStreamSynchronize(c->stream));
+            if (c->aux) HBG_TRY(hipStreamSynchronize(c->aux));  // a forked launch may still read it
             HBG_TRY(hipFree(b.p));
             b.p = nullptr;
             b.cap = 0;
@@ -308,6 +312,12 @@ void hbg_free(hbg_ctx* c) {
     for (auto& kv : c->enc_plans) (void)hipFree(kv.second);
     (void)hipFree(c->d_err);
     if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
+    if (c->aux) {
+        (void)hipStreamSynchronize(c->aux);
+        (void)hipStreamDestroy(c->aux);
+    }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -321,6 +331,23 @@ static int switch_stream(hbg_ctx* c, hipStream_t s) {
     HBG_TRY(hipEventRecord(c->switch_ev, c->stream));
     HBG_TRY(hipStreamWaitEvent(s, c->switch_ev, 0));
     c->stream = s;
+    return HBG_OK;
+}
+
+// Fork: c->aux starts after everything enqueued on c->stream so far; join:
+// c->stream continues after everything enqueued on c->aux.  For independent,
+// latency-bound launches of one call (few items: each kernel fills a few waves).
+static int fork_aux(hbg_ctx* c) {
+    if (!c->aux) HBG_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    if (!c->fork_ev) HBG_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    if (!c->join_ev) HBG_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+    HBG_TRY(hipEventRecord(c->fork_ev, c->stream));
+    HBG_TRY(hipStreamWaitEvent(c->aux, c->fork_ev, 0));
+    return HBG_OK;
+}
+static int join_aux(hbg_ctx* c) {
+    HBG_TRY(hipEventRecord(c->join_ev, c->aux));
+    HBG_TRY(hipStreamWaitEvent(c->stream, c->join_ev, 0));
     return HBG_OK;
 }
 
@@ -939,10 +966,14 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_CHECK(stage_out(c, flags, 35, plaintext, vlen, &dpt));
     HBG_CHECK(stage_out(c, flags, 36, status, 4ull * n_ct, &dst));
     HBG_CHECK(stage_out(c, flags, 37, outcome, n, &doc));
-    // set_ciphertext: Ciphertext::verify on the prepared table
+    // set_ciphertext: Ciphertext::verify on the prepared table — on the aux
+    // stream, concurrent with the share verification below (both only read
+    // the prepared table; for an epoch's few ciphertexts each is a handful of
+    // waves whose time is one pairing check's latency)
     void *ctok, *pairs, *okb, *sel;
     HBG_CHECK(scratch(c, 30, n_ct, &ctok));
-    HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok, c->stream));
+    HBG_CHECK(fork_aux(c));
+    HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok, c->aux));
     // verify_decryption_share of every (ct, sender) share, batched
     HBG_CHECK(scratch(c, 15, 8ull * n, &pairs));
     HBG_CHECK(scratch(c, 31, n, &okb));
@@ -959,6 +990,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
                                                tab.coefH, tab.coefW, (const uint32_t*)paff, (const int32_t*)pst,
                                                (uint8_t*)okb, c->stream));
     }
+    HBG_CHECK(join_aux(c));  // ct_verify's verdicts are read by tdec_select
     // handle_message / try_output: the first t+1 valid arrivals, faults, late shares
     HBG_CHECK(scratch(c, 38, (4 + 48) * m * n_ct + 4ull * n_ct, &sel));
     uint32_t* sidx = (uint32_t*)sel;

@@ -261,12 +261,12 @@ __global__ __launch_bounds__(64) void tdec_v_digest(uint64_t n, const uint8_t* _
 //   pi+chi each lane gathers the rotated words of its pi source and of the
 //          sources of (x+1, y), (x+2, y) and applies chi,
 //   iota   lane 0 only (a lane mask ANDed with the round constant),
-// ~35 VALU + 18 cross-lane gathers per round instead of the 190-instruction
-// round of one lane.  Blocks are absorbed by lanes 0..16 (8 message bytes
+// ~35 VALU + 18 cross-lane gathers (three dependent gather stages) per round
+// instead of the 190-instruction round of one lane: 4.4 us per permutation
+// against 8.8 (gathering C[x-1] and C[x+1] from the 10 lanes of the two
+// columns in ONE stage, 26 gathers per round, measured slower:
+// profiles/r03n/theta_ab.txt).  Blocks are absorbed by lanes 0..16 (8 message bytes
 // each, the next block's dwords prefetched during the current permutation).
-#ifndef HBG_VDIG_THETA1
-#define HBG_VDIG_THETA1 0
-#endif
 constexpr uint8_t kRhoOff[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39,
                                  41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
@@ -286,12 +286,6 @@ __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8
 #pragma unroll
     for (int j = 0; j < 4; ++j) col[j] = x + 5 * ((y + 1 + j) % 5);
     const uint32_t cm1 = (x + 4) % 5 + 5 * y, cp1 = (x + 1) % 5 + 5 * y;
-    uint32_t cmcol[5], cpcol[5];  // the lanes of columns x-1 and x+1
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        cmcol[j] = (x + 4) % 5 + 5 * j;
-        cpcol[j] = (x + 1) % 5 + 5 * j;
-    }
     // B[X][Y] = rho(A[x][y]) with X = y, Y = 2x + 3y: the source of (X, Y) is
     // x = 3 (Y - 3X) mod 5, y = X
     auto pisrc = [](uint32_t X, uint32_t Y) { return (3 * (Y + 15 - 3 * X)) % 5 + 5 * X; };
@@ -301,18 +295,6 @@ __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8
     uint32_t lo = 0, hi = 0;
     auto permute = [&]() {
         for (int rnd = 0; rnd < 24; ++rnd) {
-#if HBG_VDIG_THETA1
-            // C[x-1] and C[x+1] straight from the 10 lanes of the two columns:
-            // one gather stage instead of two
-            uint32_t mlo = 0, mhi = 0, plo = 0, phi = 0;
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                mlo ^= lane_get(lo, cmcol[j]);
-                mhi ^= lane_get(hi, cmcol[j]);
-                plo ^= lane_get(lo, cpcol[j]);
-                phi ^= lane_get(hi, cpcol[j]);
-            }
-#else
             uint32_t clo = lo, chi = hi;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -321,7 +303,6 @@ __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8
             }
             const uint32_t mlo = lane_get(clo, cm1), mhi = lane_get(chi, cm1);
             const uint32_t plo = lane_get(clo, cp1), phi = lane_get(chi, cp1);
-#endif
             lo = __builtin_amdgcn_bitop3_b32(lo, mlo, __builtin_amdgcn_alignbit(plo, phi, 31), 0x96);
             hi = __builtin_amdgcn_bitop3_b32(hi, mhi, __builtin_amdgcn_alignbit(phi, plo, 31), 0x96);
             uint64_t w = ((uint64_t)hi << 32) | lo;
