@@ -101,7 +101,7 @@ __device__ __forceinline__ u32x2_a4 payload_window(const EncodeRows& r, uint32_t
     return u32x2_a4{v[0], v[1]};
 }
 
-template <int D, int Q, int MODE, bool RING_DATA = false>
+template <int D, int Q, int MODE>
 struct EncodeCtx {
     const EncodeRows& r;
     u32x2_a4 buf[kPrefetch];
@@ -134,7 +134,6 @@ struct EncodeCtx {
         }
         if constexpr (MODE != 0)
             __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), 0);
-        if constexpr (RING_DATA) r.ring[(J - D) * (int)r.rdw] = w;  // data rows sit below the parity rows
         return w;
     }
 
@@ -166,9 +165,9 @@ struct EncodeCtx {
 // Column p0 + t of every row: data words (MODE 1/2: from the payload, stored
 // to the data rows) and the Q parity words.
 // RING: the parity words also go to the fused kernel's LDS ring (r.ring).
-template <int D, int Q, int MODE, bool RING = false, bool RING_DATA = false>
+template <int D, int Q, int MODE, bool RING = false>
 __device__ __forceinline__ void encode_word(const EncodeRows& r) {
-    EncodeCtx<D, Q, MODE, RING_DATA> cx{r, {}};
+    EncodeCtx<D, Q, MODE> cx{r, {}};
     uint32_t acc[Q];
 #pragma unroll
     for (int k = 0; k < Q; ++k) acc[k] = 0u;
@@ -531,9 +530,17 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
 //                far have completed is absorbed (Keccak-f, keccak_asm.h) —
 //                parity rows read it from the LDS ring (the transpose column ->
 //                row happens in LDS, parity bytes never come back from memory),
-//                data rows from the shard rows just stored (sc1 loads served by
-//                L2: the vector L1 may hold a stale copy of a line touched
-//                before the pass wrote it).
+//                data rows straight from the payload (a data row is payload
+//                bytes at a per-row offset: 18 loads + v_alignbyte per block,
+//                L2-resident since the encoder loaded the same lines one pass
+//                earlier), except the blocks that touch the length prefix or
+//                the zero padding, read back from the shard row just stored
+//                (sc1 loads served by L2: the vector L1 may hold a stale copy of
+//                a line touched before the pass wrote it).
+// Measured alternatives (profiles/r03ij, 8,192 x 1 MiB): every data row read
+// back from the shard rows 27.8 ms (26.6 as here), all 64 rows in the ring
+// 33.5 ms (26 KB LDS per wave: 6 waves per CU), waves_per_eu(3) 37.6 ms
+// (spills), no payload prefetch 27.6 ms.
 // Ring: R bytes per parity row, R a multiple of 136 (a block never wraps),
 // R >= one pass + the previous pass's unabsorbed tail (< 136), R/8 odd (a
 // ds_read_b64 of R-strided rows hits 64 distinct banks per 32-lane group).
@@ -547,24 +554,6 @@ __host__ __device__ constexpr uint32_t fused_ring_bytes(uint32_t pass_bytes) {
     return r;
 }
 
-// Where the absorb of a data row reads its block: 0 the shard row just stored
-// (sc1 loads), 1 (default) the payload itself for blocks inside it (per-lane
-// unaligned: 18 loads + v_alignbyte; L2-resident, the encoder loaded the same
-// lines one pass earlier), 2 the LDS ring (all N rows in the ring).  Measured
-// at 8,192 x 1 MiB (profiles/r03i): 27.8 / 26.6 / 33.5 ms — the ring of all
-// rows halves the waves a CU holds (26 KB of LDS per wave).
-#ifndef HBG_FUSED_DATA_SRC
-#define HBG_FUSED_DATA_SRC 1
-#endif
-// waves per SIMD the fused kernel's register budget is sized for, and
-// whether the next pass's payload windows are prefetched into registers
-#ifndef HBG_FUSED_WPE
-#define HBG_FUSED_WPE 2
-#endif
-#ifndef HBG_FUSED_PREFETCH
-#define HBG_FUSED_PREFETCH 1
-#endif
-constexpr int kFusedDataSrc = HBG_FUSED_DATA_SRC;
 
 template <int D, int Q>
 struct FusedShape {
@@ -574,11 +563,10 @@ struct FusedShape {
     static constexpr uint32_t IPB = BLK / LPI;
     static constexpr uint32_t NODES = merkle_nodes(N);
     static constexpr uint32_t R = fused_ring_bytes(4 * LPI);  // ring bytes per parity row
-    static constexpr uint32_t RROWS = kFusedDataSrc == 2 ? D + Q : Q;  // rows kept in the ring
-    static constexpr uint32_t RING = IPB * RROWS * R;
+    static constexpr uint32_t RING = IPB * Q * R;  // the parity rows
     static constexpr uint32_t TREE = IPB * NODES * 32;
     static constexpr uint32_t LDS = RING > TREE ? RING : TREE;
-    static constexpr int WPE = HBG_FUSED_WPE;  // waves per SIMD the register budget is sized for
+    static constexpr int WPE = 2;  // waves per SIMD the register budget is sized for
 };
 
 template <int D, int Q>
@@ -602,13 +590,12 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     // is left unwritten (no shards, no levels)
     const bool live = inst < n && payload_fits(P, pstride, D, L);
     uint8_t* base = shards + inst * (uint64_t)N * S;
-    constexpr uint32_t RD = kFusedDataSrc == 2 ? (uint32_t)D : 0u;  // ring row of parity row 0
-    uint32_t* ring = ring_all + sub * (F::RROWS * R / 4) + RD * (R / 4);  // this instance's parity row 0
+    uint32_t* ring = ring_all + sub * (Q * R / 4);  // this instance's parity rows
     uint32_t* tree = tree_all + sub * NODES * 8;
     const uint64_t cols = (L + 3) / 4;
     const uint32_t passes = (uint32_t)((cols + LPI - 1) / LPI);
     const bool row_lane = live && t < N;
-    const bool ring_lane = row_lane && (kFusedDataSrc == 2 || t >= (uint32_t)D);
+    const bool ring_lane = row_lane && t >= (uint32_t)D;
     // buffer resources over the workgroup's first instance (uniform); a lane's
     // instance and column / row are VGPR offsets (host: IPB * N * S and
     // IPB * pstride < 2^31)
@@ -635,7 +622,7 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             const uint32_t rp = (136u * done) % R / 8;
 #pragma unroll
             for (int i = 0; i < 17; ++i) w[i] = rrow[rp + i];
-        } else if (kFusedDataSrc == 1 && (uint64_t)t * L + 136ull * done >= 4 &&
+        } else if ((uint64_t)t * L + 136ull * done >= 4 &&
                    (uint64_t)t * L + 136ull * done + 140 <= P + 4) {
             // data row t's block is payload bytes [o, o + 136), o = t L + 136 done - 4:
             // 35 dwords from the dword below o, then a per-lane byte shift
@@ -672,13 +659,12 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         if (wpos >= R) wpos -= R;
         r.ring = ring + wpos / 4;
         if (live) {
-            constexpr bool RDATA = kFusedDataSrc == 2;
             if (have_pre) {
-                encode_word<D, Q, 3, true, RDATA>(r);
+                encode_word<D, Q, 3, true>(r);
             } else if (interior(ps)) {
-                encode_word<D, Q, 2, true, RDATA>(r);
+                encode_word<D, Q, 2, true>(r);
             } else if (4 * (uint64_t)p < L) {
-                encode_word<D, Q, 1, true, RDATA>(r);
+                encode_word<D, Q, 1, true>(r);
             }
         }
         // the pass's stores are complete in L2 (data rows) and in LDS (parity
@@ -687,7 +673,7 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         __syncthreads();
         const uint64_t written = 4ull * LPI * (ps + 1);
         const uint64_t avail = written < L ? written : L;
-        const bool next_pre = HBG_FUSED_PREFETCH && live && ps + 1 < passes && interior(ps + 1);
+        const bool next_pre = live && ps + 1 < passes && interior(ps + 1);
         have_pre = false;
         auto prefetch = [&]() {
             if (next_pre && !have_pre) {
