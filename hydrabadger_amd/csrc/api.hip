@@ -26,7 +26,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 44;
+constexpr int kNumSlots = 46;
 
 struct Buf {
     void* p = nullptr;
@@ -628,10 +628,16 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     t.coefH = (uint32_t*)ph;
     t.coefW = (uint32_t*)pwc;
     HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
-    void* pdg;
+    void *pdg, *pws;
     HBG_CHECK(scratch(c, 40, 32ull * n_ct, &pdg));
+    HBG_CHECK(scratch(c, 44, 4ull * n_ct, &pws));
+    // W's half (decode + lines) on the aux stream, beside SHA3(V) + hash_g1_g2 + H's lines
+    HBG_CHECK(fork_aux(c));
+    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, (int32_t*)pws, t.coefW, c->aux));
     HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW,
                                         (uint8_t*)pdg, c->stream));
+    HBG_CHECK(join_aux(c));
+    HBG_TRY(bls::launch_tdec_status_or(n_ct, t.ct_status, (const int32_t*)pws, c->stream));
     return HBG_OK;
 }
 

@@ -22,6 +22,9 @@ constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G
 constexpr uint32_t kResidentBlocks = 2048;
 
 // vdig: [n][32] scratch for SHA3(V) of the items with |V| > 64 (tdec_v_digest)
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
+                                    uint32_t* coefW, hipStream_t st);
+hipError_t launch_tdec_status_or(uint32_t n, int32_t* status, const int32_t* other, hipStream_t st);
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
                                   uint32_t* coefW, uint8_t* vdig, hipStream_t st);

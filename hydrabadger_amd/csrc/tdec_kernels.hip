@@ -643,13 +643,11 @@ TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
     G1A u;
     G2A w;
     if (!g1_decompress(U48 + 48ull * k, u, true)) st = HBG_E_INVALID_POINT;
-    if (!g2_decompress(W96 + 96ull * k, w, true)) st = HBG_E_INVALID_POINT;
     uint32_t* cu = ct_u + 32ull * k;
     store_fp(cu, u.x);
     store_fp(cu + 12, u.y);
     cu[24] = u.inf ? 1u : 0u;
-    cu[25] = w.inf ? 1u : 0u;
-    ct_status[k] = st;
+    ct_status[k] = st;  // W's verdict is or-ed in by tdec_status_or after tdec_ct_prepare_w
     if (st != 0) return;
     // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
     const uint64_t off = V_off[k], len = V_off[k + 1] - off;
@@ -659,7 +657,26 @@ TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
     sha3_bytes(m, ml, seed);
     const G2A h = hash_g2_from_seed(seed);
     g2_prepare(h.x, h.y, coefH + (uint64_t)k * 72 * kMillerSteps);
-    if (!w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
+}
+
+// The W half of ciphertext preparation (decode + subgroup check + the
+// G2Prepared lines of W): independent of V, so it runs on a second stream
+// while SHA3(V) and hash_g1_g2 run (stage_ct in api.hip).
+TDEC_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
+                                   int32_t* __restrict__ w_status, uint32_t* __restrict__ coefW) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    G2A w;
+    const bool ok = g2_decompress(W96 + 96ull * k, w, true);
+    ct_u[32ull * k + 25] = w.inf ? 1u : 0u;
+    w_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
+    if (ok && !w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
+}
+
+__global__ __launch_bounds__(256) void tdec_status_or(uint32_t n, int32_t* __restrict__ status,
+                                                      const int32_t* __restrict__ other) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n && status[k] == 0) status[k] = other[k];
 }
 
 TDEC_KERNEL void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
@@ -2131,6 +2148,18 @@ hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t*
     HBG_COUNT_MARK("tdec_ct_prepare", st);
     tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, vdig, W96, ct_u, ct_status, coefH,
                                                               coefW);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
+                                    uint32_t* coefW, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_ct_prepare_w", st);
+    if (n == 0) return hipSuccess;
+    tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, W96, ct_u, w_status, coefW);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_status_or(uint32_t n, int32_t* status, const int32_t* other, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    tdec_status_or<<<dim3((n + 255) / 256), dim3(256), 0, st>>>(n, status, other);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
