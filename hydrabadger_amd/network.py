@@ -68,8 +68,10 @@ def proof_index_map(n: int) -> tuple[np.ndarray, np.ndarray]:
 def all_gather_rows(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """Rank-major concatenation of every rank's equally shaped tensor along
     dim 0: one all_gather_into_tensor (RCCL over xGMI with backend "nccl"; the
-    same call under gloo in the CPU rehearsals)."""
-    if world == 1:
+    same call under gloo in the CPU rehearsals).  Without a process group the
+    tensor is returned as is; a one-rank group still runs the collective (the
+    one-GPU box's check of the RCCL branch)."""
+    if world == 1 and not dist.is_initialized():
         return t
     out = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, t.contiguous(), group=group)
@@ -256,8 +258,6 @@ class SpanningEpoch:
         return range(self.rank * self.m, (self.rank + 1) * self.m)
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
-            return t
         return all_gather_rows(t, self.world, self.group)
 
     def run(self, payloads, epoch: int = 0) -> EpochResult:

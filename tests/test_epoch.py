@@ -99,6 +99,28 @@ def test_epoch_world1_oracle_engine(name, N, P):
     assert res.exchange_bytes == 0
 
 
+def test_epoch_gloo_world1_group_runs_the_collective():
+    """A one-rank process group takes the all_gather_into_tensor branch (the
+    path the GPU test drives through RCCL) and agrees with the oracle."""
+    from tests.oracle_engine import OracleEngine
+    dist.init_process_group("gloo", rank=0, world_size=1, store=dist.HashStore())
+    try:
+        calls = []
+        real = dist.all_gather_into_tensor
+        def spy(*a, **k):
+            calls.append(1)
+            return real(*a, **k)
+        dist.all_gather_into_tensor = spy
+        try:
+            res = hbe.HoneyBadgerEpoch(7, 24, OracleEngine(), seed=2).run(epoch=1, faults=_faults(FAULTS["faulty"], hbe))
+        finally:
+            dist.all_gather_into_tensor = real
+        assert calls
+        compare(res, oep.run_epoch(7, 24, seed=2, epoch=1, faults=_faults(FAULTS["faulty"], oep)), 24)
+    finally:
+        dist.destroy_process_group()
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -149,6 +171,27 @@ def test_epoch_device_world1(name, N, P):
         compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep)), P)
     finally:
         eng.ctx.close()
+
+
+@pytest.mark.gpu
+def test_epoch_device_rccl_world1():
+    """The RCCL branch on hardware: a one-rank "nccl" process group, so every
+    message round goes through all_gather_into_tensor on device tensors (RCCL
+    refuses two ranks on one GPU: "Duplicate GPU detected", tools/rccl_probe.py),
+    same results as the oracle epoch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from hydrabadger_amd import network
+    dev = torch.device("cuda:0")
+    dist.init_process_group("nccl", rank=0, world_size=1, store=dist.HashStore(), device_id=dev)
+    eng = network.DeviceEngine(dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        res = hbe.HoneyBadgerEpoch(16, 300, eng, seed=2).run(epoch=1, faults=_faults(FAULTS["faulty"], hbe))
+        compare(res, oep.run_epoch(16, 300, seed=2, epoch=1, faults=_faults(FAULTS["faulty"], oep)), 300)
+    finally:
+        eng.ctx.close()
+        dist.destroy_process_group()
 
 
 @pytest.mark.gpu
