@@ -94,6 +94,7 @@ SIGNATURES = {
     "hbg_test_bls": (_i, [_vp, C.c_int, _u32, _vp, _u32, _vp, _u32]),
     "hbg_test_set_tdec_batched": (_i, [_vp, C.c_int]),
     "hbg_test_set_rbc_fused": (_i, [_vp, C.c_int]),
+    "hbg_test_set_rs_split": (_i, [_vp, C.c_int]),
 }
 
 _lib = None

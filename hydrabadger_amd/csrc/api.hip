@@ -50,6 +50,10 @@ struct hbg_ctx {
     // hbg_rbc_encode_merkle schedule (hbg_test_set_rbc_fused): 0 rs_encode_const + merkle_build, 1 the
     // fused rbc_encode_merkle, -1 (default) fused where it measured faster: (D, Q) = (22, 42), N = 64
     int rbc_fused = -1;
+    // reconstruct schedule (hbg_test_set_rs_split): 1 data rows by the
+    // run-time coder then missing parity rows by the constant encoder where one
+    // exists; 0 every missing row by the run-time coder; -1 (default) 1 for Q > 16
+    int rs_split = -1;
     int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
     hipEvent_t switch_ev = nullptr;  // hbg_set_stream: orders the new stream after the old one
     // a second stream for independent launches inside one call (fork / join by events)
@@ -223,8 +227,18 @@ int reconstruct_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* 
     const uint64_t ps = plan_stride(D, Q);
     void* plans = nullptr;
     HBG_CHECK(scratch(c, 11, ps * n, &plans));
-    HBG_TRY(launch_rs_plan(present_dev, D, Q, n, mat, (uint8_t*)plans, ps, c->stream));
+    // rse's order where a compile-time encoder exists: rebuild the missing data
+    // rows (run-time coefficients), then encode the missing parity rows from
+    // the data rows with the constant encoder (~1 op per GF MAC against ~4)
+    // (default: where the one-pass plan would outgrow one register-select tile,
+    // Q > 16 — N = 64: 12.85 -> 12.15 ms, N = 128: 17.6 -> 14.6 ms per 2,048 x
+    // 1 MiB decodes; N = 16 is faster in one pass, profiles/r03t)
+    const bool split = (c->rs_split == 1 || (c->rs_split < 0 && Q > 16)) && has_const_encoder(D, Q) &&
+                       const_encoder_fits(D, Q, S, 0, false);
+    HBG_TRY(launch_rs_plan(present_dev, D, Q, split ? D : D + Q, n, mat, (uint8_t*)plans, ps, c->stream));
     HBG_TRY(launch_rs_code_generic(shards, S, L, D + Q, D, n, (const uint8_t*)plans, ps, c->stream));
+    if (split)
+        HBG_TRY(launch_rs_encode_missing(D, Q, shards, S, L, n, present_dev, (const uint8_t*)plans, ps, c->stream));
     if (status_dev)
         HBG_TRY(hipMemcpy2DAsync(status_dev, sizeof(int32_t), plans, ps, sizeof(int32_t), n, hipMemcpyDeviceToDevice,
                                  c->stream));
@@ -1261,6 +1275,13 @@ int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
     std::lock_guard<std::mutex> g(c->mu);
     if (on < 0 || on > 3) return HBG_E_ARG;
     c->tdec_batched = on;
+    return HBG_OK;
+}
+
+int hbg_test_set_rs_split(hbg_ctx* c, int on) {
+    if (!c || on < -1 || on > 1) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->rs_split = on;
     return HBG_OK;
 }
 

@@ -83,8 +83,14 @@ hipError_t launch_rbc_trivial_status(uint64_t n, uint32_t N, const uint8_t* pres
                                      hipStream_t st);
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st);
-hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint64_t n, const uint8_t* matrix,
-                          uint8_t* plans, uint64_t plan_stride, hipStream_t st);
+// max_row: plan the missing rows below it (N: all, D: data rows only).
+hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint32_t max_row, uint64_t n,
+                          const uint8_t* matrix, uint8_t* plans, uint64_t plan_stride, hipStream_t st);
+// After a data-only plan: encode the missing parity rows from the data rows
+// (has_const_encoder(D, Q) and const_encoder_fits(D, Q, S, 0, false)).
+hipError_t launch_rs_encode_missing(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                    const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
+                                    hipStream_t st);
 hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
                                uint8_t* levels, hipStream_t st);
 hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,

@@ -90,6 +90,7 @@ struct EncodeRows {
     const u32x2_a4* pre;              // MODE 3 only: the D payload windows, loaded ahead (payload_window)
     uint32_t* ring;                   // RING only: parity row 0's word of this lane's column in the LDS ring
     uint32_t rdw;                     // RING only: dwords between consecutive parity rows of the ring
+    uint64_t miss0, miss1;            // MASKED only: bit k = parity row k is missing (stored), wave-uniform
 };
 
 // MODE 2's payload window of data row J at column p0 + t (8 bytes at the
@@ -165,7 +166,9 @@ struct EncodeCtx {
 // Column p0 + t of every row: data words (MODE 1/2: from the payload, stored
 // to the data rows) and the Q parity words.
 // RING: the parity words also go to the fused kernel's LDS ring (r.ring).
-template <int D, int Q, int MODE, bool RING = false>
+// MASKED: only the parity rows flagged in r.miss0/miss1 are stored (decode:
+// the missing parity rows; the present ones stay as received).
+template <int D, int Q, int MODE, bool RING = false, bool MASKED = false>
 __device__ __forceinline__ void encode_word(const EncodeRows& r) {
     EncodeCtx<D, Q, MODE> cx{r, {}};
     uint32_t acc[Q];
@@ -175,6 +178,9 @@ __device__ __forceinline__ void encode_word(const EncodeRows& r) {
     cx.columns(acc, std::make_integer_sequence<int, D>{});
 #pragma unroll
     for (int k = 0; k < Q; ++k) {
+        if constexpr (MASKED) {
+            if (!(((k < 64) ? (r.miss0 >> k) : (r.miss1 >> (k & 63))) & 1u)) continue;
+        }
         __builtin_amdgcn_raw_buffer_store_b32(acc[k], r.sh, r.vsh, (uint32_t)((uint64_t)(D + k) * r.S + 4 * r.p0), 0);
         if constexpr (RING) r.ring[k * r.rdw] = acc[k];
     }
@@ -223,6 +229,42 @@ __global__ __launch_bounds__(256, 4) void rs_encode_const(uint8_t* __restrict__ 
     } else {
         if (4 * (uint64_t)p < L) encode_word<D, Q, 0>(r);
     }
+}
+
+// Reconstruct's second half (rse reconstruct: missing parity rows are encoded
+// from the completed data rows): after rs_code_movrel rebuilt the missing data
+// rows of a data-only plan (rs_plan max_row = D), the compile-time encoder
+// recomputes the parity words and stores only the missing parity rows.
+// Instances whose plan failed (too few rows present) or with no missing parity
+// row exit at once.
+template <int D, int Q>
+__global__ __launch_bounds__(256, 4) void rs_encode_missing(uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+                                                         uint64_t n, uint32_t blocks_per_inst,
+                                                         const uint8_t* __restrict__ present,
+                                                         const uint8_t* __restrict__ plans, uint64_t plan_stride) {
+    const uint32_t lb = xcd_block(blockIdx.x, gridDim.x);
+    const uint64_t inst = lb / blocks_per_inst;
+    if (inst >= n) return;
+    if (reinterpret_cast<const CodePlan*>(plans + inst * plan_stride)->status != 0) return;
+    const uint8_t* pr = present + inst * (uint64_t)(D + Q) + D;
+    uint64_t m0 = 0, m1 = 0;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+        const uint64_t miss = __builtin_amdgcn_readfirstlane((uint32_t)pr[k]) == 0u;
+        if (k < 64)
+            m0 |= miss << k;
+        else
+            m1 |= miss << (k & 63);
+    }
+    if (!(m0 | m1)) return;
+    uint8_t* base = shards + inst * (uint64_t)(D + Q) * S;
+    const uint32_t blk = lb % blocks_per_inst;
+    const uint32_t p0 = blk * 256, p = p0 + threadIdx.x;
+    if (4 * (uint64_t)p >= L) return;
+    EncodeRows r{raw_rsrc(base), raw_rsrc(base), 4 * threadIdx.x, 4 * threadIdx.x, S, L, p0, threadIdx.x, base, base, 0};
+    r.miss0 = m0;
+    r.miss1 = m1;
+    encode_word<D, Q, 0, false, true>(r);
 }
 
 // Pack only (Trivial coding, N <= 3): send_shards' buffer into N rows.
@@ -302,7 +344,10 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
         uint32_t acc[kGenericTile];
 #pragma unroll
         for (int o = 0; o < (int)kGenericTile; ++o) acc[o] = 0u;
+        // wave-uniform row count of this tile: a tile of at most kMovrelSplit
+        // rows (a data-only plan: ~D/3 rows) skips the LDS rows and tables
         const uint32_t cnt = (n_out - o0) < (uint32_t)kGenericTile ? (n_out - o0) : (uint32_t)kGenericTile;
+        const bool use_lds = cnt > (uint32_t)kMovrelSplit;
         for (uint32_t j = 0; j < D; ++j) {
             const uint32_t w =
                 active ? reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p] : 0u;
@@ -314,7 +359,7 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
                 tl[e] = T.lo.t[e];
                 th[e] = T.hi.t[e];
             }
-            if (kMovrelSplit < (int)kGenericTile) {
+            if (kMovrelSplit < (int)kGenericTile && use_lds) {
 #pragma unroll
                 for (int e = 1; e < 16; ++e) {
                     tab[64 * e] = T.lo.t[e];
@@ -328,14 +373,16 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
             // kMovrelSplit select from registers (SALU + v_movrels), the rest read
             // the LDS copy: the two pipes run side by side.
 #pragma unroll
-            for (int o = 0; o < (int)kGenericTile; ++o) {
-                if (o < kMovrelSplit) {
-                    const uint32_t lo = oj[2 * o] >> 8, hi = (oj[2 * o + 1] >> 8) - 16u;
-                    acc[o] = xor3u(acc[o], tl[lo & 15u], th[hi & 15u]);
-                } else {
+            for (int o = 0; o < kMovrelSplit; ++o) {
+                const uint32_t lo = oj[2 * o] >> 8, hi = (oj[2 * o + 1] >> 8) - 16u;
+                acc[o] = xor3u(acc[o], tl[lo & 15u], th[hi & 15u]);
+            }
+            // (two straight-line bodies, no early exit: acc[] stays in VGPRs)
+            if (use_lds) {
+#pragma unroll
+                for (int o = kMovrelSplit; o < (int)kGenericTile; ++o)
                     acc[o] = xor3u(acc[o], *(lds32)(uintptr_t)(tab_addr + oj[2 * o]),
                                    *(lds32)(uintptr_t)(tab_addr + oj[2 * o + 1]));
-                }
             }
         }
         if (active) {
@@ -349,12 +396,14 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
 
 // Per-instance reconstruct plan (rse reconstruct_internal, restated):
 // rows_used = first D present rows in index order; dec = inv(M[rows_used]);
-// for every missing row r: coef[r] = M[r] * dec (so one pass rebuilds missing
-// data AND parity rows; identical bytes to rse's two-pass form because both
-// are the same linear map of the same D input rows).
+// for every missing row r < max_row: coef[r] = M[r] * dec.  max_row = N: one
+// pass rebuilds missing data AND parity rows (identical bytes to rse's
+// two-pass form: the same linear map of the same D input rows); max_row = D:
+// the missing data rows only, and rs_encode_missing then encodes the missing
+// parity rows from the completed data rows — rse's own order.
 // One 256-thread workgroup per instance; dynamic LDS: aug[D][2D] + row buffer.
 __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ present, uint32_t D, uint32_t Q,
-                                               uint64_t n, const uint8_t* __restrict__ matrix,
+                                               uint32_t max_row, uint64_t n, const uint8_t* __restrict__ matrix,
                                                uint8_t* __restrict__ plans, uint64_t plan_stride) {
     const uint64_t inst = blockIdx.x;
     if (inst >= n) return;
@@ -381,7 +430,7 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
             if (pr[i]) {
                 if (np < D) s_rows[np] = i;
                 ++np;
-            } else {
+            } else if (i < max_row) {
                 s_out[no++] = (uint8_t)i;
             }
         }
@@ -948,6 +997,25 @@ bool const_encoder_fits(uint32_t D, uint32_t Q, uint64_t S, uint64_t pstride, bo
     return has_const_encoder(D, Q) && ipb * (D + Q) * S < lim && ipb * (pstride + 16) < lim;
 }
 
+template <int D, int Q>
+static hipError_t launch_missing(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n, const uint8_t* present,
+                                 const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
+    const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    rs_encode_missing<D, Q><<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, n, bpi, present, plans,
+                                                                             plan_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_encode_missing(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                    const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
+                                    hipStream_t st) {
+    if (D == 2 && Q == 2) return launch_missing<2, 2>(shards, S, L, n, present, plans, plan_stride, st);
+    if (D == 6 && Q == 10) return launch_missing<6, 10>(shards, S, L, n, present, plans, plan_stride, st);
+    if (D == 22 && Q == 42) return launch_missing<22, 42>(shards, S, L, n, present, plans, plan_stride, st);
+    if (D == 44 && Q == 84) return launch_missing<44, 84>(shards, S, L, n, present, plans, plan_stride, st);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen,
                                   hipStream_t st) {
@@ -994,10 +1062,10 @@ hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint3
     return hipGetLastError();
 }
 
-hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint64_t n, const uint8_t* matrix,
-                          uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
+hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint32_t max_row, uint64_t n,
+                          const uint8_t* matrix, uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const size_t lds = 768 + (size_t)D * 2 * D;
-    rs_plan<<<dim3((uint32_t)n), dim3(256), lds, st>>>(present, D, Q, n, matrix, plans, plan_stride);
+    rs_plan<<<dim3((uint32_t)n), dim3(256), lds, st>>>(present, D, Q, max_row, n, matrix, plans, plan_stride);
     return hipGetLastError();
 }
 

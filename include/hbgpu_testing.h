@@ -26,6 +26,13 @@ int hbg_test_set_tdec_batched(hbg_ctx *ctx, int on);
  * where it measured faster on MI355X — (D, Q) = (22, 42), N = 64 — and two
  * launches elsewhere.  Both write identical shards and levels. */
 int hbg_test_set_rbc_fused(hbg_ctx *ctx, int on);
+/* Choose the reconstruct schedule of hbg_rs_reconstruct / hbg_rbc_decode for
+ * the (D, Q) with a compile-time coding matrix: 1 rebuild the missing data
+ * rows from the first D present rows, then encode the missing parity rows
+ * from the data rows (rse's reconstruct order); 0 rebuild every missing row in
+ * one pass of the run-time coder; -1 (the default) 1 where Q > 16, where it
+ * measured faster on MI355X.  Identical shards. */
+int hbg_test_set_rs_split(hbg_ctx *ctx, int on);
 int hbg_test_bls(hbg_ctx *ctx, int op, uint32_t n, const uint32_t *in, uint32_t in_words, uint32_t *out,
                  uint32_t out_words);
 #ifdef __cplusplus

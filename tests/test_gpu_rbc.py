@@ -387,3 +387,89 @@ def test_fused_schedule_matches_two_launch_schedule(N, P, n):
         rs, rl = corc.rbc_encode_merkle(N, pays[k].copy())
         assert np.array_equal(out[1][0][k], rs), k
         assert np.array_equal(out[1][1][k], rl), k
+
+
+@pytest.mark.parametrize("D,Q", [(2, 2), (6, 10), (22, 42), (44, 84)])
+@pytest.mark.parametrize("L", [1, 5, 257, 4099])
+def test_reconstruct_split_schedule_matches_one_pass(D, Q, L):
+    """hbg_test_set_rs_split: missing data rows by the run-time coder, then the
+    missing parity rows by the constant encoder (rse's own order) — the same
+    shards as the one-pass coder and the oracle, for erasure patterns with no
+    missing data row, no missing parity row, exactly 2f missing, too few
+    present, and a corrupted present parity row past the first D (kept as
+    received, not re-encoded)."""
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    N, n = D + Q, 8
+    data = np.frombuffer(synth.synth_bytes(synth.TAG_PAYLOAD, N * 17 + L, n * N * L), np.uint8).reshape(n, N, L).copy()
+    for k in range(n):
+        corc.rs_encode(D, Q, data[k])
+    present = np.ones((n, N), np.uint8)
+    present[1, D:] = 0                                        # parity only missing
+    present[2, :min(D, Q)] = 0                                # data only missing
+    for k in (3, 4, 5):
+        present[k] = synth.erasure_mask(77 * D + k, N, Q)     # exactly 2f missing
+    present[6] = synth.erasure_mask(91 * D, N, Q + 1)         # too few present
+    present[7] = synth.erasure_mask(93 * D, N, Q - 1)
+    last = int(np.flatnonzero(present[7])[-1])
+    assert last >= D
+    data[7, last, 0] ^= 0xFF                                  # corrupted, not among the first D present
+    outs = []
+    ctx = _lib.Context(0)
+    try:
+        for split in (0, 1):
+            _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, split))
+            dmg = data.copy()
+            dmg[present == 0] = 0xEE
+            st = bc.Coding(D, Q, ctx=ctx).reconstruct_batch(dmg, present)
+            outs.append((dmg, st))
+    finally:
+        ctx.close()
+    assert np.array_equal(outs[0][1], outs[1][1])
+    for k in range(n):
+        if present[k].sum() < D:
+            assert outs[1][1][k] == -14
+            continue
+        assert outs[1][1][k] == 0
+        ref = data[k].copy()
+        ref[present[k] == 0] = 0
+        assert corc.rs_reconstruct(D, Q, ref, present[k]) == 0
+        assert np.array_equal(outs[0][0][k], ref), (k, "one pass")
+        assert np.array_equal(outs[1][0][k], ref), (k, "split")
+
+
+@pytest.mark.parametrize("N,P,n", [(64, 1 << 20, 6), (16, 65536, 24), (128, 1 << 20, 3)])
+def test_decode_split_schedule_matches_one_pass(N, P, n):
+    """Decode (reconstruct + tree + root check + glue) at BASELINE sizes with
+    both reconstruct schedules: the same payloads, statuses and rebuilt shards."""
+    torch = _torch()
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    pay, shards, levels, L, S = _device_batch(N, P, n, first=700)
+    data, parity = bc.shard_counts(N)
+    nodes = levels.shape[1]
+    present = torch.tensor([synth.erasure_mask(700 + k, N, parity) for k in range(n)], dtype=torch.uint8,
+                           device="cuda:0")
+    roots = levels[:, nodes - 1, :].contiguous()
+    OS = (data * L + 15) // 16 * 16
+    res = []
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        for split in (0, 1):
+            _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, split))
+            dmg = shards.clone()
+            dmg[present == 0] = 0x5A
+            out = torch.zeros((n, OS), dtype=torch.uint8, device="cuda:0")
+            plen = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+            st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+            bc.rbc_decode_batch(N, L, dmg, present, roots, out, plen, st, ctx=ctx, device=True)
+            torch.cuda.synchronize()
+            res.append((dmg, out, plen, st))
+    finally:
+        ctx.close()
+    for dmg, out, plen, st in res:
+        assert st.cpu().tolist() == [1] * n
+        assert plen.cpu().tolist() == [P] * n
+        assert torch.equal(out[:, :P], pay[:, :P])
+        assert torch.equal(dmg[:, :, :L], shards[:, :, :L])

@@ -89,9 +89,12 @@ def main():
             out = torch.empty((B, OS), dtype=torch.uint8, device=dev)
             dpl = torch.empty(B, dtype=torch.int64, device=dev)
             dst = torch.empty(B, dtype=torch.uint8, device=dev)
-            res["decode_ms"] = t(lambda: bc.rbc_decode_batch(N, L, shards, present, roots, out, dpl, dst, ctx=ctx,
-                                                             device=True, asynchronous=True))
-            res["decode_ok"] = bool((dst == 1).all().item())
+            for split in (0, 1):  # hbg_test_set_rs_split: one-pass coder / data rows + constant parity encoder
+                _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, split))
+                res[f"decode_split{split}_ms"] = t(lambda: bc.rbc_decode_batch(
+                    N, L, shards, present, roots, out, dpl, dst, ctx=ctx, device=True, asynchronous=True))
+                res[f"decode_split{split}_ok"] = bool((dst == 1).all().item())
+            _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, -1))
         print(json.dumps(res), flush=True)
         del pay, shards, levels
         torch.cuda.empty_cache()
