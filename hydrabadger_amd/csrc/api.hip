@@ -64,10 +64,12 @@ struct hbg_ctx {
 
 namespace {
 
-#define HBG_TRY(expr)                              \
-    do {                                           \
-        hipError_t e_ = (expr);                    \
-        if (e_ != hipSuccess) return HBG_E_DEVICE; \
+// A launcher's hipErrorInvalidConfiguration is a batch too large for one
+// grid (grid.h): an argument error, not a device fault.
+#define HBG_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) return e_ == hipErrorInvalidConfiguration ? HBG_E_ARG : HBG_E_DEVICE; \
     } while (0)
 
 #define HBG_CHECK(expr)              \

@@ -6,6 +6,7 @@
 
 #include "../../include/hbgpu.h"
 #include "dev_err.h"
+#include "grid.h"
 
 namespace hbg {
 

@@ -971,6 +971,7 @@ static hipError_t launch_encode_const(uint8_t* shards, uint64_t S, uint64_t L, u
                                       hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
     const uint64_t blocks = n * bpi;
+    HBG_GRID_CHECK(blocks, 256);
     if (payloads)
         rs_encode_const<D, Q, true><<<dim3((uint32_t)blocks), dim3(256), 0, st>>>(shards, S, L, n, bpi, payloads,
                                                                                    pstride, plen);
@@ -1001,6 +1002,7 @@ template <int D, int Q>
 static hipError_t launch_missing(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n, const uint8_t* present,
                                  const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    HBG_GRID_CHECK(n * bpi, 256);
     rs_encode_missing<D, Q><<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, n, bpi, present, plans,
                                                                              plan_stride);
     return hipGetLastError();
@@ -1031,6 +1033,7 @@ static hipError_t launch_fused(uint8_t* shards, uint64_t S, uint64_t L, uint64_t
                                uint64_t pstride, const uint64_t* plen, uint8_t* levels, hipStream_t st) {
     using F = FusedShape<D, Q>;
     const uint64_t blocks = (n + F::IPB - 1) / F::IPB;
+    HBG_GRID_CHECK(blocks, F::BLK);
     rbc_encode_merkle<D, Q><<<dim3((uint32_t)blocks), dim3(F::BLK), 0, st>>>(shards, S, L, n, payloads, pstride,
                                                                              plen, levels);
     return hipGetLastError();
@@ -1049,6 +1052,7 @@ hipError_t launch_rbc_encode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uin
 hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,
                             const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    HBG_GRID_CHECK(n * bpi, 256);
     pack_rows<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, rows, n, bpi, payloads, pstride,
                                                                plen);
     return hipGetLastError();
@@ -1057,6 +1061,7 @@ hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N,
 hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                                   const uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const uint32_t bpi = (uint32_t)(((L + 3) / 4 + 255) / 256);
+    HBG_GRID_CHECK(n * bpi, 256);
     rs_code_movrel<<<dim3((uint32_t)(n * bpi)), dim3(256), kGenericLds, st>>>(shards, S, L, N, D, n, bpi, plans,
                                                                             plan_stride);
     return hipGetLastError();
@@ -1065,6 +1070,7 @@ hipError_t launch_rs_code_generic(uint8_t* shards, uint64_t S, uint64_t L, uint3
 hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint32_t max_row, uint64_t n,
                           const uint8_t* matrix, uint8_t* plans, uint64_t plan_stride, hipStream_t st) {
     const size_t lds = 768 + (size_t)D * 2 * D;
+    HBG_GRID_CHECK(n, 256);
     rs_plan<<<dim3((uint32_t)n), dim3(256), lds, st>>>(present, D, Q, max_row, n, matrix, plans, plan_stride);
     return hipGetLastError();
 }
@@ -1077,6 +1083,7 @@ hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, ui
     const uint32_t ipb = 256 / lpi;
     const uint64_t blocks = (n + ipb - 1) / ipb;
     const size_t lds = (size_t)ipb * nodes * 32;
+    HBG_GRID_CHECK(blocks, 256);
     merkle_build<<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
     return hipGetLastError();
 }
@@ -1085,6 +1092,7 @@ hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* value
                                   const uint32_t* index, const uint8_t* digests, uint32_t depth,
                                   const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
                                   hipStream_t st) {
+    HBG_GRID_CHECK((n + 255) / 256, 256);
     merkle_validate<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index, digests,
                                                                            depth, ndig, roots, ok, n);
     return hipGetLastError();
@@ -1094,12 +1102,13 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
                            const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
                            uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st) {
     const uint32_t nodes = merkle_nodes(N);
+    const uint64_t maxlen = (uint64_t)D * L;
+    const uint32_t bpi = (uint32_t)(((maxlen + 15) / 16 + 255) / 256);
+    HBG_GRID_CHECK(n * bpi, 256);
     rbc_glue_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(shards, S, L, N, D, n, levels, nodes,
                                                                             roots, rstatus, plen, status);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint64_t maxlen = (uint64_t)D * L;
-    const uint32_t bpi = (uint32_t)(((maxlen + 15) / 16 + 255) / 256);
     rbc_glue_copy<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, plen, status, out,
                                                                     ostride);
     return hipGetLastError();
@@ -1108,6 +1117,7 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
 hipError_t launch_rbc_check_plen(uint64_t n, const uint64_t* plen, uint64_t pstride, uint32_t D, uint64_t L,
                                  int32_t* err, hipStream_t st) {
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK((n + 255) / 256, 256);
     rbc_check_plen<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, plen, pstride, D, L, err);
     return hipGetLastError();
 }
@@ -1115,6 +1125,7 @@ hipError_t launch_rbc_check_plen(uint64_t n, const uint64_t* plen, uint64_t pstr
 hipError_t launch_rbc_trivial_status(uint64_t n, uint32_t N, const uint8_t* present, int32_t* status,
                                      hipStream_t st) {
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK((n + 255) / 256, 256);
     rbc_trivial_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, N, present, status);
     return hipGetLastError();
 }
@@ -1122,6 +1133,7 @@ hipError_t launch_rbc_trivial_status(uint64_t n, uint32_t N, const uint8_t* pres
 hipError_t launch_synth(uint32_t tag, uint64_t first, uint64_t nbytes, uint8_t* out, uint64_t ostride, uint64_t n,
                         hipStream_t st) {
     const uint32_t bpr = (uint32_t)(((nbytes + 7) / 8 + 255) / 256);
+    HBG_GRID_CHECK(n * bpr, 256);
     synth_bytes<<<dim3((uint32_t)(n * bpr)), dim3(256), 0, st>>>(tag, first, nbytes, out, ostride, n, bpr);
     return hipGetLastError();
 }

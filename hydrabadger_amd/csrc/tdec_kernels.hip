@@ -18,6 +18,7 @@
 
 #include "bls.h"
 #include "dev_err.h"
+#include "grid.h"
 #include "keccak.h"
 #include "keccak_asm.h"
 #include "tdec_kernels.h"
@@ -2127,6 +2128,7 @@ constexpr uint64_t kVDigestWaveMax = 8192;
 hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_off, uint8_t* dig, hipStream_t st) {
     HBG_COUNT_MARK("tdec_v_digest", st);
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK((n + 63) / 64, 64);
     if (n <= kVDigestWaveMax)  // few items (the epoch's contributions): one wave per sponge
         tdec_v_digest_wave<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
     else
@@ -2137,6 +2139,7 @@ hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uin
                                      uint8_t* out, const int32_t* status, hipStream_t st) {
     HBG_COUNT_MARK("tdec_keystream_xor", st);
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK(n, 256);
     tdec_keystream_xor<<<dim3((uint32_t)n), dim3(256), 0, st>>>(n, seeds, in, off, out, status);
     return hipGetLastError();
 }
@@ -2194,6 +2197,7 @@ hipError_t launch_tdec_index_sanitize(uint64_t n, const uint32_t* a, uint32_t a_
                                       hipStream_t st) {
     HBG_COUNT_MARK("tdec_index_sanitize", st);
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK((n + 255) / 256, 256);
     tdec_index_sanitize<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, a, a_bound, b, b_bound, a_out,
                                                                                b_out, err);
     return hipGetLastError();
@@ -2295,6 +2299,7 @@ hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8
 hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st) {
     HBG_COUNT_MARK("tdec_pair_index", st);
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK((n + 255) / 256, 256);
     tdec_pair_index<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(n, N, sct, spk);
     return hipGetLastError();
 }

@@ -473,3 +473,22 @@ def test_decode_split_schedule_matches_one_pass(N, P, n):
         assert plen.cpu().tolist() == [P] * n
         assert torch.equal(out[:, :P], pay[:, :P])
         assert torch.equal(dmg[:, :, :L], shards[:, :, :L])
+
+
+def test_batch_larger_than_one_grid_is_an_argument_error():
+    """A device-mode batch whose grid would not fit one dispatch (2^32 work-
+    items) is refused with HBG_E_ARG before anything is launched, instead of
+    running on a truncated grid; the context stays usable."""
+    torch = _torch()
+    from hydrabadger_amd import _lib
+    out = torch.zeros((4, 16), dtype=torch.uint8, device="cuda:0")
+    ctx = _lib.Context(0)
+    try:
+        rc = _lib.lib().hbg_synth_bytes(ctx.h, 1, 0, 8, _lib.ptr(out), 16, 1 << 40, _lib.HBG_DEVICE)
+        assert rc == _lib.HBG_E_ARG
+        rc = _lib.lib().hbg_synth_bytes(ctx.h, 1, 0, 8, _lib.ptr(out), 16, 4, _lib.HBG_DEVICE)
+        assert rc == _lib.HBG_OK
+        torch.cuda.synchronize()
+        assert bool((out[:, :8] != 0).any())
+    finally:
+        ctx.close()
