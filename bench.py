@@ -905,7 +905,14 @@ def main():
         r = run_leg("tdec", lambda: tdec_leg(ctx, dev, a.tdec_cts, 2, seed=1 + rank))
         if r is not None:
             tdec, tdec_ep = r
-            tdec["value"] = shard.sum_over_ranks(tdec["value"], agg_dev)  # whole-job shares/s
+        # every rank joins both reductions, whether or not its leg ran (a rank
+        # that skipped a collective would leave the others waiting in it)
+        total = shard.sum_over_ranks(tdec["value"] if tdec else 0.0, agg_dev)  # whole-job shares/s
+        ranks_ok = int(round(shard.sum_over_ranks(1.0 if tdec else 0.0, agg_dev)))
+        if tdec is not None:
+            tdec["value"] = total if ranks_ok == world else None
+            if ranks_ok != world:
+                run_leg.errors["tdec_ranks"] = f"TDec leg failed on {world - ranks_ok} of {world} ranks"
 
     epoch = (run_leg("epoch", lambda: epoch_leg(ctx, dev, a.epoch_nodes, a.epoch_contrib, max(2, min(a.steps, 5)),
                                                 agg_dev))
