@@ -864,7 +864,7 @@ def main():
     # ---- decode path: reconstruct exactly 2f erasures + tree + glue ----
     def decode_leg():
         from hydrabadger_amd import workload
-        nd = min(B, 2048)
+        nd = B  # the headline batch (reconstruct + tree + glue of every instance the step encoded)
         present = torch.tensor([workload.erasure_mask(first + k, N_NODES, parity) for k in range(nd)],
                                dtype=torch.uint8, device=dev)
         roots = levels[:nd, nodes - 1, :].contiguous()
