@@ -37,6 +37,9 @@
  *    nodes = hbg_merkle_nodes(N); level l (size n_l, n_0 = N,
  *    n_{l+1} = ceil(n_l/2)) starts at sum_{m<l} n_m; the root is the last
  *    digest.  `MerkleTree::proof(i)` is a pure index walk over this array.
+ *  - One call is one set of kernel launches: a batch whose launch grid would
+ *    exceed a single dispatch (2^31 workgroups or 2^32 work-items, e.g. ~16 M
+ *    tiny-payload instances) returns HBG_E_ARG before anything runs; split it.
  *  - No callbacks; no allocation is returned to the caller.
  */
 #ifndef HBGPU_H
