@@ -12,6 +12,7 @@
 
 #include <initializer_list>
 #include <map>
+#include <functional>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -686,9 +687,13 @@ bool use_batched(const hbg_ctx* c, uint64_t n) {
     return c->tdec_batched >= 2 || n >= kBatchMinShares;
 }
 
+// after_leaves (optional): enqueues work that should start once the leaves
+// are done (ThresholdDecrypt's Ciphertext::verify on the second stream, so it
+// shares the chip with the check rounds instead of stalling the leaves).
 int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uint8_t* dU48, uint32_t n,
                           uint32_t n_pk, const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp,
-                          const uint32_t* paff, const int32_t* pst, uint8_t* dok) {
+                          const uint32_t* paff, const int32_t* pst, uint8_t* dok,
+                          const std::function<int()>& after_leaves = {}) {
     uint32_t* tbl = nullptr;
     if (c->tdec_batched == 2 || (uint64_t)n >= kPkTableMinUses * n_pk) {
         void* p;
@@ -767,6 +772,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.ct_status, paff, pst, tbl,
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream));
     HBG_DBG_STEP(c, "batch_leaves");
+    if (after_leaves) HBG_CHECK(after_leaves());
     // round 0: every batch sum; failing batches push their 16-share groups
     HBG_TRY(bls::launch_tdec_batch_check(nb, counts + 3, nullptr, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it1,
                                          counts, (uint32_t*)fails, counts + 1, c->stream));
@@ -990,12 +996,21 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_CHECK(stage_out(c, flags, 37, outcome, n, &doc));
     // set_ciphertext: Ciphertext::verify on the prepared table — on the aux
     // stream, concurrent with the share verification below (both only read
-    // the prepared table; for an epoch's few ciphertexts each is a handful of
-    // waves whose time is one pairing check's latency)
+    // the prepared table).  For an epoch's few ciphertexts each is a handful
+    // of waves whose time is one pairing check's latency: forked at once.  On
+    // the batched path it is forked after the leaves launch: a ct_verify grid
+    // that fills the chip would otherwise hold the leaves back until it
+    // drains, while next to the check rounds it takes their idle slots.
     void *ctok, *pairs, *okb, *sel;
     HBG_CHECK(scratch(c, 30, n_ct, &ctok));
-    HBG_CHECK(fork_aux(c));
-    HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok, c->aux));
+    auto ct_verify = [&]() -> int {
+        HBG_CHECK(fork_aux(c));
+        HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok,
+                                           c->aux));
+        return HBG_OK;
+    };
+    const bool batched = use_batched(c, n);
+    if (!batched) HBG_CHECK(ct_verify());
     // verify_decryption_share of every (ct, sender) share, batched
     HBG_CHECK(scratch(c, 15, 8ull * n, &pairs));
     HBG_CHECK(scratch(c, 31, n, &okb));
@@ -1004,9 +1019,9 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_TRY(bls::launch_tdec_pair_index(n, n_nodes, sct, spk, c->stream));
     void *paff, *pst;
     HBG_CHECK(prepare_pks(c, n_nodes, (const uint8_t*)dpk, &paff, &pst));
-    if (use_batched(c, n)) {
+    if (batched) {
         HBG_CHECK(verify_shares_batched(c, n_ct, tab, tab.U48, (uint32_t)n, n_nodes, (const uint8_t*)dsh, sct, spk,
-                                        (const uint32_t*)paff, (const int32_t*)pst, (uint8_t*)okb));
+                                        (const uint32_t*)paff, (const int32_t*)pst, (uint8_t*)okb, ct_verify));
     } else {
         HBG_TRY(bls::launch_tdec_verify_shares(n, nullptr, (const uint8_t*)dsh, sct, spk, tab.ct_u, tab.ct_status,
                                                tab.coefH, tab.coefW, (const uint32_t*)paff, (const int32_t*)pst,
