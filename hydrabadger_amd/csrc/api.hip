@@ -60,6 +60,7 @@ struct hbg_ctx {
     // a second stream for independent launches inside one call (fork / join by events)
     hipStream_t aux = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    bool aux_open = false;  // forked and not yet joined (AuxJoin closes it on every return path)
     std::mutex mu;
 };
 
@@ -360,13 +361,24 @@ static int fork_aux(hbg_ctx* c) {
     if (!c->join_ev) HBG_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
     HBG_TRY(hipEventRecord(c->fork_ev, c->stream));
     HBG_TRY(hipStreamWaitEvent(c->aux, c->fork_ev, 0));
+    c->aux_open = true;
     return HBG_OK;
 }
 static int join_aux(hbg_ctx* c) {
     HBG_TRY(hipEventRecord(c->join_ev, c->aux));
     HBG_TRY(hipStreamWaitEvent(c->stream, c->join_ev, 0));
+    c->aux_open = false;
     return HBG_OK;
 }
+// Scope guard of a forking call: a call that returns early (an error between
+// fork and join) still orders its stream after the aux work, so the next call
+// cannot reuse scratch the aux stream is still writing.
+struct AuxJoin {
+    hbg_ctx* c;
+    ~AuxJoin() {
+        if (c->aux_open) (void)join_aux(c);
+    }
+};
 
 int hbg_set_stream(hbg_ctx* c, void* s) {
     if (!c) return HBG_E_ARG;
@@ -649,6 +661,7 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     HBG_CHECK(scratch(c, 40, 32ull * n_ct, &pdg));
     HBG_CHECK(scratch(c, 44, 4ull * n_ct, &pws));
     // W's half (decode + lines) on the aux stream, beside SHA3(V) + hash_g1_g2 + H's lines
+    AuxJoin guard{c};
     HBG_CHECK(fork_aux(c));
     HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, (int32_t*)pws, t.coefW, c->aux));
     HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW,
@@ -1003,6 +1016,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     // drains, while next to the check rounds it takes their idle slots.
     void *ctok, *pairs, *okb, *sel;
     HBG_CHECK(scratch(c, 30, n_ct, &ctok));
+    AuxJoin guard{c};
     auto ct_verify = [&]() -> int {
         HBG_CHECK(fork_aux(c));
         HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok,
