@@ -794,6 +794,8 @@ def main():
 
     from hydrabadger_amd import _lib, shard
     from hydrabadger_amd import broadcast as bc
+    if os.environ.get("HBG_LAT_LANES"):  # A/B knob of the BLS latency build (hbgpu_testing.h); default untouched
+        _lib.lib().hbg_test_set_latency_lanes(int(os.environ["HBG_LAT_LANES"]))
 
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(dev)  # one dedicated stream: events and engine launches share it

@@ -26,7 +26,9 @@ CFLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fconstexpr-s
 
 
 def _deps_mtime(src: str) -> float:
-    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(PKG, "..", "include", "*.h"))
+    # a translation unit may include another .hip (tdec_kernels_lat.hip)
+    hdrs = (glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.hip")) +
+            glob.glob(os.path.join(PKG, "..", "include", "*.h")))
     return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in hdrs])
 
 

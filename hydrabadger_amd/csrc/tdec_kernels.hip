@@ -14,6 +14,8 @@
 //   tdec_combine        PublicKeySet::decrypt: interpolate the first t+1 shares
 //                       at 0 (Lagrange over Fr) + xor_with_hash
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stdint.h>
 
 #include "bls.h"
@@ -2159,6 +2161,62 @@ TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
 }
 
 // ------------------------------------------------------------------ launchers
+// Latency build: tdec_kernels_lat.hip compiles this file a second time into
+// namespace bls_lat with HBG_FP_LAT (three interleaved accumulators per Fp
+// multiplication column, bls_fp_mul.h).  Launches of at most kLatLanes lanes
+// (<= one wave per SIMD slot at this occupancy: the epoch's 128 ciphertexts,
+// a few thousand messages) take those kernels — a lone wave's multiplication
+// is a dependency chain — and larger ones the serial chain, which issues
+// fewer instructions.
+#if HBG_TDEC_LAT_TU || defined(HBG_FP_COUNT) || defined(HBG_DEBUG_CHECKS)
+// (the latency build itself, and the instrumented / diagnostic tool builds:
+// every launch stays in this build so counts and checks see all of it)
+#define HBG_LAT_DISPATCH(lanes, call) ((void)0)
+#else
+}  // namespace bls
+namespace bls_lat {
+hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                                  const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
+                                  uint32_t* coefW, uint8_t* vdig, hipStream_t st);
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
+                                    uint32_t* coefW, hipStream_t st);
+hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
+                                  hipStream_t st);
+hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
+                                     const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
+                                     const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
+                                     const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
+                                     const uint32_t* sel);
+hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
+                                 const uint32_t* coefW, uint8_t* ok, hipStream_t st);
+hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
+                               const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
+                               uint32_t* scratch, uint8_t* seeds, hipStream_t st);
+hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
+                           const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st);
+hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
+                             const uint32_t* msg_pk, const uint8_t* msg, const uint64_t* off, const uint8_t* sig96,
+                             uint32_t* lines, uint8_t* ok, int32_t* err, hipStream_t st);
+hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
+                                     const uint32_t* frame_pk, const uint8_t* frames, const uint64_t* off,
+                                     uint32_t* lines, int32_t* status, hipStream_t st);
+hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
+                               const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
+                               uint8_t* seeds, uint8_t* vdig, int32_t* est, int32_t* err, hipStream_t st);
+hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, const uint32_t* u_aff,
+                                     const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
+                                     const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
+                                     hipStream_t st);
+}  // namespace bls_lat
+namespace bls {
+// 2,048 waves of 64 lanes: two per SIMD, the TDec kernels' occupancy
+// (hbg_test_set_latency_lanes overrides it: the parity tests run both builds)
+std::atomic<uint64_t> g_lat_lanes{64ull * 2048};
+#define HBG_LAT_DISPATCH(lanes, call)                                                           \
+    do {                                                                                        \
+        if ((uint64_t)(lanes) <= g_lat_lanes.load(std::memory_order_relaxed)) return ::hbg::bls_lat::call; \
+    } while (0)
+#endif
 #ifdef HBG_FP_COUNT
 // Instrumented builds (tools/fpcount.py): every launcher first closes the
 // previous launch's count (stream sync + read/clear of g_fp_count) and
@@ -2215,6 +2273,7 @@ hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uin
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
                                   uint32_t* coefW, uint8_t* vdig, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare(n, U48, V, V_off, W96, ct_u, ct_status, coefH, coefW, vdig, st));
     hipError_t e = launch_tdec_v_digest(n, V, V_off, vdig, st);
     if (e != hipSuccess) return e;
     HBG_COUNT_MARK("tdec_ct_prepare", st);
@@ -2224,6 +2283,7 @@ hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t*
 }
 hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
                                     uint32_t* coefW, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare_w(n, W96, ct_u, w_status, coefW, st));
     HBG_COUNT_MARK("tdec_ct_prepare_w", st);
     if (n == 0) return hipSuccess;
     tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, W96, ct_u, w_status, coefW);
@@ -2236,6 +2296,7 @@ hipError_t launch_tdec_status_or(uint32_t n, int32_t* status, const int32_t* oth
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_pk_prepare(n, pk48, pk_aff, pk_status, st));
     HBG_COUNT_MARK("tdec_pk_prepare", st);
     tdec_pk_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, pk48, pk_aff, pk_status);
     return hipGetLastError();
@@ -2254,6 +2315,7 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
                                      const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
                                      const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
                                      const uint32_t* sel) {
+    HBG_LAT_DISPATCH(cap, launch_tdec_verify_shares(cap, n_dev, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok, st, sel));
     HBG_COUNT_MARK("tdec_verify_shares", st);
     if (cap == 0) return hipSuccess;
     tdec_verify_shares<<<item_grid(cap), dim3(64), 0, st>>>(cap, n_dev, share48, share_ct, share_pk, ct_u,
@@ -2380,6 +2442,7 @@ hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32
 }
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_verify(n, ct_u, ct_status, coefH, coefW, ok, st));
     HBG_COUNT_MARK("tdec_ct_verify", st);
     tdec_ct_verify<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, ct_u, ct_status, coefH, coefW, ok);
     return hipGetLastError();
@@ -2387,6 +2450,7 @@ hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, uint8_t* seeds, hipStream_t st) {
+    HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 32 ? 32u : 64u), launch_tdec_combine(n, t, share48, idx, V, V_off, out, status, scratch, seeds, st));
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     if (t + 1 <= 32)
@@ -2403,6 +2467,7 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
 static dim3 grid64(uint64_t n) { return dim3((uint32_t)((n + 63) / 64)); }
 hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
                            const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_bls_sign(n, n_sk, sk32, msg_sk, msg, off, sig96, err, st));
     HBG_COUNT_MARK("bls_sign", st);
     if (n == 0) return hipSuccess;
     bls_sign<<<grid64(n), dim3(64), 0, st>>>(n, n_sk, sk32, msg_sk, msg, off, sig96, err);
@@ -2411,6 +2476,7 @@ hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const
 hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
                              const uint32_t* msg_pk, const uint8_t* msg, const uint64_t* off, const uint8_t* sig96,
                              uint32_t* lines, uint8_t* ok, int32_t* err, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_bls_verify(n, n_pk, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok, err, st));
     HBG_COUNT_MARK("bls_verify", st);
     if (n == 0) return hipSuccess;
     bls_verify<<<grid64(n), dim3(64), 0, st>>>(n, n_pk, pk_aff, pk_status, msg_pk, msg, off, sig96, lines, ok, err);
@@ -2419,6 +2485,7 @@ hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, 
 hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,
                                      const uint32_t* frame_pk, const uint8_t* frames, const uint64_t* off,
                                      uint32_t* lines, int32_t* status, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_wire_verify_frames(n, pk_aff, pk_status, n_pk, frame_pk, frames, off, lines, status, st));
     HBG_COUNT_MARK("wire_verify_frames", st);
     if (n == 0) return hipSuccess;
     wire_verify_frames<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, n_pk, frame_pk, frames, off, lines,
@@ -2428,6 +2495,7 @@ hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const i
 hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, const uint8_t* r32,
                                const uint8_t* msg, const uint64_t* off, uint8_t* U48, uint8_t* V, uint8_t* W96,
                                uint8_t* seeds, uint8_t* vdig, int32_t* est, int32_t* err, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_encrypt(n, pk_aff, pk_status, r32, msg, off, U48, V, W96, seeds, vdig, est, err, st));
     HBG_COUNT_MARK("tdec_encrypt", st);
     if (n == 0) return hipSuccess;
     tdec_encrypt_u<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, r32, U48, W96, seeds, est, err);
@@ -2443,6 +2511,7 @@ hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, c
                                      const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
                                      const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
                                      hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_decrypt_share(n, n_ct, n_sk, u_aff, u_status, sk32, share_ct, share_sk, share48, status, err, st));
     HBG_COUNT_MARK("tdec_decrypt_share", st);
     if (n == 0) return hipSuccess;
     tdec_decrypt_share<<<grid64(n), dim3(64), 0, st>>>(n, n_ct, n_sk, u_aff, u_status, sk32, share_ct, share_sk,
@@ -2524,6 +2593,7 @@ hipError_t launch_sig_verify_shares(uint64_t cap, const uint32_t* n_dev, const u
 }  // namespace hbg
 
 #ifdef HBG_FP_COUNT
+#if !HBG_TDEC_LAT_TU  // one definition: the throughput build reports its own launches
 extern "C" int hbg_fp_count_report(char* buf, uint64_t cap) {
     using namespace hbg::bls;
     count_mark(nullptr, nullptr);
@@ -2539,5 +2609,19 @@ extern "C" int hbg_fp_count_report(char* buf, uint64_t cap) {
     if (js.size() + 1 > cap) return -1;
     memcpy(buf, js.c_str(), js.size() + 1);
     return 0;
+}
+#endif
+#endif
+
+#if !HBG_TDEC_LAT_TU
+// hbgpu_testing.h: launches of at most `lanes` lanes take the latency build
+// (0: none, UINT64_MAX: all); returns the previous value.
+extern "C" uint64_t hbg_test_set_latency_lanes(uint64_t lanes) {
+#if defined(HBG_FP_COUNT) || defined(HBG_DEBUG_CHECKS)
+    (void)lanes;
+    return 0;
+#else
+    return hbg::bls::g_lat_lanes.exchange(lanes);
+#endif
 }
 #endif

@@ -22,6 +22,16 @@ from tests.tdec_fixtures import from_limbs, limbs, scenario
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["latency-build", "throughput-build"], autouse=True)
+def _bls_build(request):
+    """Every test here runs on both builds of the BLS12-381 kernels (same
+    results; hbgpu_testing.h hbg_test_set_latency_lanes)."""
+    from hydrabadger_amd import _lib
+    prev = _lib.lib().hbg_test_set_latency_lanes((1 << 64) - 1 if request.param == "latency-build" else 0)
+    yield
+    _lib.lib().hbg_test_set_latency_lanes(prev)
+
+
 def _th():
     from hydrabadger_amd import threshold as th
     return th

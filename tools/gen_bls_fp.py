@@ -161,11 +161,19 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--acc", type=int, default=1, help="accumulators per column (1 = the serial chain)")
-    K = ap.parse_args().acc
-    if K <= 1:
-        body = gen_mul("fp_mul_raw", False) + gen_mul("fp_sqr_raw", True)
-    else:
-        body = gen_mul_k("fp_mul_raw", False, K) + gen_mul_k("fp_sqr_raw", True, K)
+    ap.add_argument("--lat-acc", type=int, default=3,
+                    help="accumulators per column of the latency build (HBG_FP_LAT, tdec_kernels_lat.hip)")
+    a = ap.parse_args()
+
+    def variant(K):
+        if K <= 1:
+            return gen_mul("fp_mul_raw", False) + gen_mul("fp_sqr_raw", True)
+        return gen_mul_k("fp_mul_raw", False, K) + gen_mul_k("fp_sqr_raw", True, K)
+    # The throughput build (every kernel of the product library) runs the
+    # serial chain; the latency build — the same BLS kernels compiled a second
+    # time for launches of at most a couple of thousand waves — interleaves
+    # lat-acc independent accumulators per column.
+    body = ("#if HBG_FP_LAT\n" + variant(a.lat_acc) + "#else\n" + variant(a.acc) + "#endif\n\n")
     path = os.path.join(ROOT, "hydrabadger_amd", "csrc", "bls_fp_mul.h")
     with open(path, "w") as f:
         f.write("".join(hdr) + body + "}  // namespace bls\n}  // namespace hbg\n")
