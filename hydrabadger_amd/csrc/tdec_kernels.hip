@@ -2207,6 +2207,8 @@ hipError_t launch_tdec_decrypt_share(uint64_t n, uint32_t n_ct, uint32_t n_sk, c
                                      const int32_t* u_status, const uint8_t* sk32, const uint32_t* share_ct,
                                      const uint32_t* share_sk, uint8_t* share48, int32_t* status, int32_t* err,
                                      hipStream_t st);
+hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t* off, uint32_t* coefH,
+                                  uint8_t* seeds, hipStream_t st);
 }  // namespace bls_lat
 namespace bls {
 // 2,048 waves of 64 lanes: two per SIMD, the TDec kernels' occupancy
@@ -2540,6 +2542,7 @@ hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* ou
 
 hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t* off, uint32_t* coefH,
                                   uint8_t* seeds, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_sig_doc_prepare(n, doc, off, coefH, seeds, st));
     HBG_COUNT_MARK("sig_doc_prepare", st);
     if (n == 0) return hipSuccess;
     sig_doc_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, doc, off, coefH, seeds);
