@@ -632,6 +632,44 @@ BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool us
     return fp12_is_one(f);
 }
 
+// The same check for Jacobian G1 points P = (X, Y, Z), Z != 0, without the two
+// inversions of a conversion to affine: each line value at (X/Z^2, Y/Z^3) is
+// taken times Z^3 (c2 Z^3 + c1 XZ + c0 Y), an Fp factor that the final
+// exponentiation maps to 1 ((p - 1) divides (p^12 - 1) / r).  Inputs: XZ, Y, Z^3.
+BD void ell_jac(Fp12* f, const LineCoeff& c, const Fp& xz, const Fp& y, const Fp& z3) {
+    const Fp2 c0 = fp2_mul_fp(c.c2, z3), c1 = fp2_mul_fp(c.c1, xz), c4 = fp2_mul_fp(c.c0, y);
+    fp12_mul_by_014_p(f, &c0, &c1, &c4);
+}
+__device__ __noinline__ void miller_loop2_jac(Fp12* out, const uint32_t* c1, Fp p1xz, Fp p1y, Fp p1z3, bool use1,
+                                              const uint32_t* c2, Fp p2xz, Fp p2y, Fp p2z3, bool use2) {
+    Fp12 f = fp12_one();
+    int k = 0;
+    for (int i = 61; i >= 0; --i) {
+        if (use1) ell_jac(&f, load_line(c1 + 72 * k), p1xz, p1y, p1z3);
+        if (use2) ell_jac(&f, load_line(c2 + 72 * k), p2xz, p2y, p2z3);
+        ++k;
+        if ((kXHalf >> i) & 1ull) {
+            if (use1) ell_jac(&f, load_line(c1 + 72 * k), p1xz, p1y, p1z3);
+            if (use2) ell_jac(&f, load_line(c2 + 72 * k), p2xz, p2y, p2z3);
+            ++k;
+        }
+        fp12_sqr_p(&f, &f);
+    }
+    if (use1) ell_jac(&f, load_line(c1 + 72 * k), p1xz, p1y, p1z3);
+    if (use2) ell_jac(&f, load_line(c2 + 72 * k), p2xz, p2y, p2z3);
+    *out = fp12_conj(f);
+}
+// e(P1, Q1) e(P2, Q2) == 1 for Jacobian P1, P2 (an identity point: its pair is skipped)
+BD bool pairing_check2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2, const G1& p2, bool use2) {
+    const bool u1 = !fp_is_zero(p1.z), u2 = use2 && !fp_is_zero(p2.z);
+    const Fp z1 = fp_sqr(p1.z), z2 = fp_sqr(p2.z);
+    Fp12 f;
+    miller_loop2_jac(&f, c1, fp_mul(p1.x, p1.z), p1.y, fp_mul(z1, p1.z), u1, c2, fp_mul(p2.x, p2.z), p2.y,
+                     fp_mul(z2, p2.z), u2);
+    final_exponentiation(&f);
+    return fp12_is_one(f);
+}
+
 // ------------------------------------------------------------------ kernels
 TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
                                                       const uint8_t* __restrict__ V,
@@ -1030,11 +1068,12 @@ TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_d
     const uint32_t l0 = node_first(it.node);
     if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;  // nothing valid to vouch for: those shares stay 0
     const uint32_t* sm = sums + (uint64_t)it.b * kBatchSumWords + it.node * kSumWords;
-    const G1A a = g1_to_affine(load_jac(sm)), bb = g1_to_affine(load_jac(sm + kJacWords));
+    const G1 a = load_jac(sm), bj = load_jac(sm + kJacWords);
     const bool w_inf = ct_u[32ull * d.ct + 25] != 0;
-    const bool pass = pairing_check2(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a.x, a.y, !a.inf,
-                                     coefW + (uint64_t)d.ct * kLineWordsPerPoint, bb.x, fp_neg(bb.y),
-                                     !bb.inf && !w_inf);
+    // e(sum r S, H) e(-sum r PK, W) == 1, on the Jacobian sums directly
+    const bool pass = pairing_check2_jac(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a,
+                                         coefW + (uint64_t)d.ct * kLineWordsPerPoint, {bj.x, fp_neg(bj.y), bj.z},
+                                         !w_inf);
     batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n);
 }
 
@@ -2163,11 +2202,12 @@ TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
 // ------------------------------------------------------------------ launchers
 // Latency build: tdec_kernels_lat.hip compiles this file a second time into
 // namespace bls_lat with HBG_FP_LAT (three interleaved accumulators per Fp
-// multiplication column, bls_fp_mul.h).  Launches of at most kLatLanes lanes
-// (<= one wave per SIMD slot at this occupancy: the epoch's 128 ciphertexts,
-// a few thousand messages) take those kernels — a lone wave's multiplication
-// is a dependency chain — and larger ones the serial chain, which issues
-// fewer instructions.
+// multiplication column, bls_fp_mul.h) and one wave per SIMD's register
+// budget.  Launches of at most g_lat_lanes lanes (one wave per SIMD: the
+// epoch's 128 ciphertexts, up to ~65 k messages) take those kernels — a lone
+// wave's multiplication is a dependency chain, and its scratch round trips
+// are what a larger register budget removes — and larger ones the serial
+// chain at two waves per SIMD, which issues fewer instructions.
 #if HBG_TDEC_LAT_TU || defined(HBG_FP_COUNT) || defined(HBG_DEBUG_CHECKS)
 // (the latency build itself, and the instrumented / diagnostic tool builds:
 // every launch stays in this build so counts and checks see all of it)
@@ -2211,9 +2251,9 @@ hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t
                                   uint8_t* seeds, hipStream_t st);
 }  // namespace bls_lat
 namespace bls {
-// 2,048 waves of 64 lanes: two per SIMD, the TDec kernels' occupancy
+// 1,024 waves of 64 lanes: one per SIMD, the latency build's occupancy
 // (hbg_test_set_latency_lanes overrides it: the parity tests run both builds)
-std::atomic<uint64_t> g_lat_lanes{64ull * 2048};
+std::atomic<uint64_t> g_lat_lanes{64ull * 1024};
 #define HBG_LAT_DISPATCH(lanes, call)                                                           \
     do {                                                                                        \
         if ((uint64_t)(lanes) <= g_lat_lanes.load(std::memory_order_relaxed)) return ::hbg::bls_lat::call; \

@@ -35,11 +35,11 @@ int hbg_test_set_rbc_fused(hbg_ctx *ctx, int on);
 int hbg_test_set_rs_split(hbg_ctx *ctx, int on);
 /* The BLS12-381 kernels exist in two builds with identical results: the
  * throughput build (serial multiply-accumulate chain per Fp multiplication
- * column) and the latency build (three interleaved chains, fewer dependent
- * stalls for a lone wave, ~8 % more instructions).  Launches of at most
- * `lanes` work-items take the latency build (default 131,072 = two waves per
- * SIMD; 0: never; UINT64_MAX: always).  Process-wide; returns the previous
- * value. */
+ * column, two waves per SIMD) and the latency build (three interleaved chains
+ * and one wave per SIMD's register budget: fewer dependent stalls and spills
+ * for a lone wave).  Launches of at most `lanes` work-items take the latency
+ * build (default 65,536 = one wave per SIMD; 0: never; UINT64_MAX: always).
+ * Process-wide; returns the previous value. */
 uint64_t hbg_test_set_latency_lanes(uint64_t lanes);
 int hbg_test_bls(hbg_ctx *ctx, int op, uint32_t n, const uint32_t *in, uint32_t in_words, uint32_t *out,
                  uint32_t out_words);
