@@ -211,16 +211,17 @@ TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_prepare", "tdec_ct_verify", "
 def tdec_pmc_traffic(n_shares: int) -> dict:
     """HBM bytes of one ThresholdDecrypt call at the bench shape (100k x 64,
     1 % bad), from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE per kernel, profiles/r03/pmc_tdec_100k.json); almost all of it
+    WRITE_SIZE per kernel, profiles/r03al/pmc_tdec_100k.json, HEAD of round 3
+    with the bucket-MSM combine); almost all of it
     is the kernels' scratch (spill / call-frame) traffic, since a share is 48 B."""
-    path = os.path.join(ROOT, "profiles", "r03", "pmc_tdec_100k.json")
+    path = os.path.join(ROOT, "profiles", "r03al", "pmc_tdec_100k.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return {}
     per_kernel = {}
     for name, v in d.items():
-        short = name.split("::")[-1]
+        short = name.split("::")[-1].split("<")[0]
         if short in TDEC_DRIVER_KERNELS and isinstance(v, dict) and "hbm_read_bytes_corrected" in v:
             per_kernel[short] = v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
     if not per_kernel or n_shares != 6_400_000:
@@ -228,7 +229,7 @@ def tdec_pmc_traffic(n_shares: int) -> dict:
     total = sum(per_kernel.values())
     return {"bytes_per_call": total, "bytes_per_share": total / n_shares,
             "per_kernel_bytes_per_share": {k: v / n_shares for k, v in sorted(per_kernel.items(), key=lambda x: -x[1])},
-            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh via tools/gpu_r03al.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                       "passes over tools/tdec_kbench.py --cts 100000)"}
 
 
