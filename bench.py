@@ -748,6 +748,22 @@ def init_distributed(backend: str, local: int):
     return world, rank
 
 
+def dist_info(dist: bool) -> dict:
+    """What the process group actually saw (not what was asked for): backend,
+    ranks in the group, and the RCCL version when the backend is nccl."""
+    if not dist:
+        return {"backend": None, "world_size_seen": 1, "rccl_version": None}
+    backend = torch.distributed.get_backend()
+    ver = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            ver = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception as e:  # report, never fail the line on it
+            ver = f"unavailable: {e}"
+    return {"backend": backend, "world_size_seen": torch.distributed.get_world_size(), "rccl_version": ver}
+
+
 def run_timed(step, steps: int, warmup: int, sync, agg_dev) -> float:
     """W untimed steps, then exactly K steps bracketed by a barrier and a
     device sync on both sides; the max over ranks of the wall time (s)."""
@@ -948,6 +964,7 @@ def main():
             "tdec_inputs": tdec_in,
             "coin": coin,
             "leg_errors": run_leg.errors or None,
+            "distributed": dist_info(dist),
         }
         print(json.dumps(line), flush=True)
     ctx.close()

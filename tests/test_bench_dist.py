@@ -36,6 +36,8 @@ def _rank(rank, world, port, q):
         dt = bench.run_timed(step, 3, 2, lambda: None, torch.device("cpu"))
         from hydrabadger_amd import shard
         total = shard.sum_over_ranks(float(rank + 1), torch.device("cpu"))
+        info = bench.dist_info(True)
+        assert info == {"backend": "gloo", "world_size_seen": world, "rccl_version": None}
         q.put((rank, dt, len(calls), total))
     finally:
         torch.distributed.destroy_process_group()
@@ -69,6 +71,10 @@ def test_legs_record_failures_and_keep_going():
     assert legs("b", boom) is None
     assert legs("c", lambda: 3) == 3
     assert legs.errors == {"b": "RuntimeError: HIP error: device lost"}
+
+
+def test_dist_info_single_process():
+    assert bench.dist_info(False) == {"backend": None, "world_size_seen": 1, "rccl_version": None}
 
 
 def test_bench_backend_switch_parses():
