@@ -124,6 +124,30 @@ def pmc_traffic(instances: int) -> dict:
     return out
 
 
+# Kernels of one hbg_rbc_decode call at N = 64 (PMC passes: tools/gpu_r04a.sh,
+# profiles/r04/pmc_decode_8192.json; FETCH_SIZE x2 + WRITE_SIZE per kernel).
+DECODE_KERNELS = ("rs_plan", "rs_code_movrel", "rs_encode_missing", "merkle_build", "rbc_glue_status",
+                  "rbc_glue_copy", "rbc_decode_merkle")
+
+
+def decode_pmc_traffic(instances: int) -> dict:
+    path = os.path.join(ROOT, "profiles", "r04", "pmc_decode_8192.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+    if instances != 8192:
+        return {}
+    by = {}
+    for name, v in d.items():
+        short = name.split("<")[0]
+        if short in DECODE_KERNELS and "hbm_read_bytes_corrected" in v:
+            by[short] = v["hbm_read_bytes_corrected"] + v.get("hbm_write_bytes", 0.0)
+    if not by:
+        return {}
+    return {"bytes_per_call": sum(by.values()), "by_kernel": by, "source": os.path.relpath(path, ROOT)}
+
+
 def timed(fn, reps: int):
     """Average ms per call of fn over reps (events on the current stream)."""
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -155,7 +179,7 @@ def cpu_baseline(n_sample: int):
 
 # TDec roofline constants.  Every Fp multiplication / squaring the kernels run
 # is a generated 12x12-limb Montgomery CIOS body of 288 v_mad_u64_u32
-# (tools/gen_bls_fp.py; counted in the gfx950 asm).  The peak is the measured
+# (tools/gen_bls_fp_sub.py: the hbg_fpmul1/2/3 subroutines; counted in the gfx950 asm).  The peak is the measured
 # v_mad_u64_u32 issue rate — 4.44 cycles per wave-instruction per SIMD at 8
 # waves/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) — at the 2.4 GHz
 # nominal clock on 1,024 SIMDs: 35.4 T lane-MADs/s.
@@ -213,10 +237,11 @@ TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_prepare", "tdec_ct_verify", "
 def tdec_pmc_traffic(n_shares: int) -> dict:
     """HBM bytes of one ThresholdDecrypt call at the bench shape (100k x 64,
     1 % bad), from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE per kernel, profiles/r03al/pmc_tdec_100k.json, HEAD of round 3
-    with the bucket-MSM combine); almost all of it
-    is the kernels' scratch (spill / call-frame) traffic, since a share is 48 B."""
-    path = os.path.join(ROOT, "profiles", "r03al", "pmc_tdec_100k.json")
+    WRITE_SIZE per kernel, profiles/r04/pmc_tdec_100k.json: the register-
+    resident tower of round 4); most of it is still scratch (the final
+    exponentiation's parked Fp12 values, the G2 steps' call frames), since a
+    share is 48 B."""
+    path = os.path.join(ROOT, "profiles", "r04", "pmc_tdec_100k.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -231,14 +256,14 @@ def tdec_pmc_traffic(n_shares: int) -> dict:
     total = sum(per_kernel.values())
     return {"bytes_per_call": total, "bytes_per_share": total / n_shares,
             "per_kernel_bytes_per_share": {k: v / n_shares for k, v in sorted(per_kernel.items(), key=lambda x: -x[1])},
-            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh via tools/gpu_r03al.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                      "passes over tools/tdec_kbench.py --cts 100000)"}
+            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh via tools/gpu_r04c.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                      "passes over tools/tdec_kbench.py --cts 100000, register-resident tower)"}
 
 
 def fp_count_floor() -> dict:
     """The batched verifier's executed Fp count with no bad share (no group
-    testing, no per-share fallback): profiles/r03/fpcount_batched_0pct.json."""
-    path = os.path.join(ROOT, "profiles", "r03", "fpcount_batched_0pct.json")
+    testing, no per-share fallback): profiles/r04/fpcount_batched_0pct.json."""
+    path = os.path.join(ROOT, "profiles", "r04", "fpcount_batched_0pct.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -704,10 +729,17 @@ def epoch_leg(ctx, dev, n_nodes: int, contrib: int, reps: int, agg_dev):
     """configs[4]: one HoneyBadger epoch of ONE n_nodes-node network whose
     nodes are split over all ranks (hydrabadger_amd/epoch.py): threshold-
     encrypt every contribution, the Broadcast Value -> Echo -> Ready rounds as
-    bincode wire messages (each round one all-gather, RCCL over xGMI), decode,
-    and ThresholdDecrypt of every accepted ciphertext (shares exchanged by one
-    more all-gather).  Timed per phase on every rank, max over ranks; every
-    contribution must come out of ThresholdDecrypt byte-exact."""
+    bincode wire messages (Values by one all-to-all to their recipients,
+    Echoes / Readys / decryption shares by all-gathers: RCCL over xGMI),
+    decode, and ThresholdDecrypt of every accepted ciphertext.  The headline
+    epoch is per-node faithful: every node validates the Values addressed to
+    it and every echo, decodes every instance and runs its own
+    ThresholdDecrypt of every accepted ciphertext with its own arrival order
+    (the network's whole crypto work, spread over the ranks); the shared view
+    (one check / decode / TDec instance per rank for all its nodes) is timed
+    beside it, labelled as such.  Timed per phase on every rank, max over
+    ranks; every contribution must come out of every node's ThresholdDecrypt
+    byte-exact."""
     from hydrabadger_amd import epoch as hbe
     from hydrabadger_amd import network, shard
     eng = network.DeviceEngine(dev, ctx)
@@ -716,28 +748,43 @@ def epoch_leg(ctx, dev, n_nodes: int, contrib: int, reps: int, agg_dev):
     def check(res, e):
         want = eng.synth(hbe.TAG_CONTRIB, hbe.instance_id(e, 0), n_nodes, contrib)
         return (bool(res.delivered.all()) and res.accepted == list(range(n_nodes))
-                and bool((res.ct_status == 0).all()) and bool(torch.equal(res.plaintexts, want)))
-    ok = check(ep.run(epoch=0), 0)  # warm
-    phases = {}
-    for r in range(reps):
-        if torch.distributed.is_initialized():
-            torch.distributed.barrier()
-        res = ep.run(epoch=1 + r)
-        ok = ok and check(res, 1 + r)
-        for k, v in res.times_ms.items():
-            phases[k] = phases.get(k, 0.0) + v / reps
-    phases = {k: shard.max_over_ranks(v, agg_dev) for k, v in phases.items()}
+                and bool((res.ct_status == 0).all())
+                and all(bool(torch.equal(res.plaintexts[v], want)) for v in range(len(res.views))))
+
+    def timed_epochs(per_node: bool):
+        ok = check(ep.run(epoch=0, per_node=per_node), 0)  # warm
+        phases = {}
+        for r in range(reps):
+            if torch.distributed.is_initialized():
+                torch.distributed.barrier()
+            res = ep.run(epoch=1 + r, per_node=per_node)
+            ok = ok and check(res, 1 + r)
+            for k, v in res.times_ms.items():
+                phases[k] = phases.get(k, 0.0) + v / reps
+        return {k: shard.max_over_ranks(v, agg_dev) for k, v in phases.items()}, res, ok
+    phases, res, ok = timed_epochs(True)
+    torch.cuda.empty_cache()
+    sphases, sres, sok = timed_epochs(False)
     f = (n_nodes - 1) // 3
+    work = {k: int(shard.sum_over_ranks(float(v), agg_dev)) for k, v in res.work.items()}
     return {"workload": f"one {n_nodes}-node HoneyBadger epoch (RS {n_nodes - 2 * f}+{2 * f}, t={f}), "
                         f"{contrib}-B contributions threshold-encrypted and broadcast, nodes split over "
-                        f"{ep.world} rank(s)",
+                        f"{ep.world} rank(s); per-node faithful (every node's own validations, decodes and "
+                        f"ThresholdDecrypt)",
             "nodes_per_rank": ep.m, "epoch_ms": phases["epoch"], "phases_ms": phases,
             "contributions_per_s": n_nodes / (phases["epoch"] * 1e-3),
             "contribution_GBps": n_nodes * contrib / (phases["epoch"] * 1e-3) / 1e9,
-            "allgather_recv_bytes_per_rank": res.exchange_bytes,
+            "network_work_per_epoch": work,
+            "share_verifications_per_s": work.get("tdec_shares", 0) / (phases["tdec"] * 1e-3),
+            "collective_recv_bytes_per_rank": res.exchange_bytes,
             "messages_per_epoch": {"value": n_nodes * n_nodes, "echo": n_nodes * n_nodes,
                                    "ready": n_nodes * n_nodes, "decryption_shares": n_nodes * n_nodes},
-            "all_decrypted_ok": ok}
+            "all_decrypted_ok": ok,
+            "shared_view": {"note": "one check / decode / ThresholdDecrypt instance per rank on behalf of all its "
+                                    "nodes (round 3's epoch): not the network's work",
+                            "epoch_ms": sphases["epoch"], "phases_ms": sphases,
+                            "work": {k: int(shard.sum_over_ranks(float(v), agg_dev)) for k, v in sres.work.items()},
+                            "all_decrypted_ok": sok}}
 
 
 def init_distributed(backend: str, local: int):
@@ -904,8 +951,26 @@ def main():
         torch.cuda.synchronize()
         ok = bool((st == 1).all().item()) and bool(torch.equal(out[:, :PAYLOAD], pay[:nd]))
         ms_dec = timed(dec, reps)
+        # Roofline (DESIGN.md §4 "decode"): exactly Q = 2f rows are rebuilt from
+        # the first D present rows, so the coding work is Q x D x L/4 MAC-words,
+        # the encoder's, and the Merkle rebuild hashes all N rows: the same
+        # 109.1 M lane-ops per instance as send_shards.  Algorithmic bytes: read
+        # the D present rows, write the Q rebuilt rows, the tree and the payload.
+        d_ops = ops + enc_ops
+        d_bytes = data * L + parity * L + (2 * N_NODES - 1) * 32 + PAYLOAD
+        achieved = d_ops * nd / (ms_dec * 1e-3)
+        tr = decode_pmc_traffic(nd)
         return {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
-                "erased_per_instance": parity, "roundtrip_ok": ok}
+                "erased_per_instance": parity, "roundtrip_ok": ok,
+                "roofline": {"bound": "valu", "unit": "Tops/s", "achieved": achieved / 1e12,
+                             "peak": VALU_PEAK / 1e12, "frac": achieved / VALU_PEAK,
+                             "alg_ops_per_instance": d_ops, "alg_bytes_per_instance": d_bytes,
+                             "hbm": {"achieved_GBps": d_bytes * nd / (ms_dec * 1e-3) / 1e9,
+                                     "frac": d_bytes * nd / (ms_dec * 1e-3) / HBM_PEAK},
+                             "traffic": tr.get("bytes_per_call"), "traffic_unit": "HBM bytes per decode call (PMC)",
+                             "traffic_vs_alg_bytes": (tr["bytes_per_call"] / (d_bytes * nd)
+                                                      if tr.get("bytes_per_call") else None),
+                             "traffic_by_kernel": tr.get("by_kernel"), "traffic_source": tr.get("source")}}
 
     decode = run_leg("decode", decode_leg) if not a.no_decode and "decode" in legs else None
     bwire = (run_leg("bwire", lambda: broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps))

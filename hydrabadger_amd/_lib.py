@@ -55,6 +55,7 @@ _vp, _u8p, _u32, _u64, _i = C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_
 SIGNATURES = {
     "hbg_init": (_i, [C.POINTER(C.c_void_p), _i]),
     "hbg_free": (None, [_vp]),
+    "hbg_ctx_device": (_i, [_vp]),
     "hbg_set_stream": (_i, [_vp, _vp]),
     "hbg_reset_stream": (_i, [_vp]),
     "hbg_sync": (_i, [_vp]),
@@ -146,6 +147,7 @@ class Context:
         h = C.c_void_p()
         check(lib().hbg_init(C.byref(h), device), "hbg_init")
         self.h = h
+        self.device = lib().hbg_ctx_device(h)   # the device it binds (device -1: the current one)
 
     def close(self) -> None:
         if self.h:
@@ -183,7 +185,8 @@ def default_context() -> Context:
         _default = Context()
     torch = sys.modules.get("torch")
     if torch is not None and torch.cuda.is_initialized():
-        h = torch.cuda.current_stream().cuda_stream
+        # the current stream of the context's device (not of torch's current device)
+        h = torch.cuda.current_stream(_default.device).cuda_stream
         if h != _default_stream:
             _default.set_stream(h)
             _default_stream = h

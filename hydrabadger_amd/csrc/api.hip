@@ -66,12 +66,16 @@ struct hbg_ctx {
 
 namespace {
 
-// A launcher's hipErrorInvalidConfiguration is a batch too large for one
-// grid (grid.h): an argument error, not a device fault.
-#define HBG_TRY(expr)                                                                    \
-    do {                                                                                 \
-        hipError_t e_ = (expr);                                                          \
-        if (e_ != hipSuccess) return e_ == hipErrorInvalidConfiguration ? HBG_E_ARG : HBG_E_DEVICE; \
+// A batch too large for one grid is refused by the launchers' own guard
+// (grid.h, before anything of the call is enqueued): an argument error.  Any
+// other failure, a runtime launch-configuration error included, is a device
+// error.
+#define HBG_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return (e_ == hipErrorInvalidConfiguration && ::hbg::take_grid_refused()) ? HBG_E_ARG \
+                                                                                     : HBG_E_DEVICE; \
     } while (0)
 
 #define HBG_CHECK(expr)              \
@@ -386,10 +390,20 @@ int hbg_set_stream(hbg_ctx* c, void* s) {
     return switch_stream(c, (hipStream_t)s);
 }
 
+int hbg_ctx_device(const hbg_ctx* c) { return c ? c->device : -1; }
+
 int hbg_reset_stream(hbg_ctx* c) {
     if (!c) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    return switch_stream(c, c->own);
+    if (switch_stream(c, c->own) == HBG_OK) return HBG_OK;
+    // the external stream could not be ordered (e.g. destroyed before the
+    // reset): fall back to a device-wide synchronisation, so the context can
+    // always get back to its own stream
+    (void)hipGetLastError();
+    HBG_TRY(hipSetDevice(c->device));
+    HBG_TRY(hipDeviceSynchronize());
+    c->stream = c->own;
+    return HBG_OK;
 }
 
 int hbg_sync(hbg_ctx* c) {
@@ -908,6 +922,7 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
     if (!c || (n_ct && (!share48 || !idx || !V_off || !out || !status))) return HBG_E_ARG;
     if (n_ct == 0) return HBG_OK;
     if (t >= 4096) return HBG_E_ARG;  // far beyond any N <= 65536 network; bounds the per-lane scratch
+    if (!grid_fits(n_ct, 64)) return HBG_E_ARG;  // refused before anything is staged or launched
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t m = (uint64_t)t + 1;
@@ -1115,6 +1130,7 @@ int hbg_tdec_encrypt(hbg_ctx* c, const uint8_t* pk48, uint64_t n, const uint8_t*
                      const uint64_t* msg_off, uint8_t* U48, uint8_t* V, uint8_t* W96, uint32_t flags) {
     if (!c || (n && (!pk48 || !r32 || !msg_off || !U48 || !W96))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
+    if (!grid_fits((n + 63) / 64, 64)) return HBG_E_ARG;  // refused before anything is staged or launched
     std::lock_guard<std::mutex> g(c->mu);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];

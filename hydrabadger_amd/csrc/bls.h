@@ -7,10 +7,14 @@
 // intermediate can be unit-tested against oracle/bls12_381.py.
 //
 // gfx950 mapping
-//  * Fp = 12 x u32 limbs as an ext_vector so it travels in VGPRs across
-//    calls; fp_mul / fp_sqr are the only non-inlined primitives (one ~650-op
-//    body each: 288 v_mad_u64_u32 + 288 v_addc, see tools/gen_bls_fp.py),
-//    everything above them inlines, keeping code size bounded.
+//  * Fp = 12 x u32 limbs as an ext_vector so it travels in VGPRs.  The
+//    Montgomery multiplications are the only out-of-line code: fixed-register
+//    leaf subroutines (bls_fp_sub.h, tools/gen_bls_fp_sub.py: 288
+//    v_mad_u64_u32 + 288 carry counts per product, 1, 2 or 3 independent
+//    products interleaved per call) entered by an inline-asm s_swappc whose
+//    clobber list names exactly the registers they write — so everything
+//    above them inlines and stays in registers across the calls (the standard
+//    call ABI would clobber ~150 VGPRs per multiplication).
 //  * Fp2 / Fp6 / Fp12 are plain structs of Fp; exponentiations run rolled
 //    loops over constant exponent words (scalar loads, wave-uniform branches).
 #pragma once
@@ -18,12 +22,10 @@
 #include <stdint.h>
 
 #include "bls_consts.h"
-#include "bls_fp_mul.h"
+#include "bls_fp_sub.h"
 
 namespace hbg {
 namespace bls {
-
-typedef uint32_t Fp __attribute__((ext_vector_type(12)));
 
 #define BD __device__ __forceinline__
 
@@ -60,31 +62,46 @@ __device__ __forceinline__ void fp_count(int which) {
 #define HBG_FP_COUNT_CALL(which) ((void)0)
 #endif
 
-__device__ __noinline__ Fp fp_mul(Fp a, Fp b) {
+// Montgomery products through the fixed-register subroutines: the operands
+// are bound to the subroutine's input VGPRs, results come back over the
+// first operands, the temporaries are clobbers (the asm is not volatile, so
+// identical products may be merged by the compiler).
+BD Fp fp_mul(Fp a, Fp b) {
     HBG_FP_COUNT_CALL(0);
-    uint32_t x[12], y[12], r[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        x[i] = a[i];
-        y[i] = b[i];
-    }
-    fp_mul_raw(r, x, y);
-    Fp o;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) o[i] = r[i];
-    return o;
+    asm(HBG_FP_SUB_CALL("hbg_fpmul1") : "+{v[0:11]}"(a) : "{v[12:23]}"(b) : HBG_FP_SUB1_CLOBBERS);
+    return a;
 }
 
-__device__ __noinline__ Fp fp_sqr(Fp a) {
+BD Fp fp_sqr(Fp a) {
     HBG_FP_COUNT_CALL(1);
-    uint32_t x[12], r[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) x[i] = a[i];
-    fp_sqr_raw(r, x);
-    Fp o;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) o[i] = r[i];
-    return o;
+    asm(HBG_FP_SUB_CALL("hbg_fpmul1") : "+{v[0:11]}"(a) : "{v[12:23]}"(a) : HBG_FP_SUB1_CLOBBERS);
+    return a;
+}
+
+// (a0 b0, a1 b1): two independent products in one interleaved call
+BD void fp_mul2(Fp& r0, Fp& r1, Fp a0, Fp b0, Fp a1, Fp b1) {
+    HBG_FP_COUNT_CALL(0);
+    HBG_FP_COUNT_CALL(0);
+    asm(HBG_FP_SUB_CALL("hbg_fpmul2")
+        : "+{v[0:11]}"(a0), "+{v[24:35]}"(a1)
+        : "{v[12:23]}"(b0), "{v[36:47]}"(b1)
+        : HBG_FP_SUB2_CLOBBERS);
+    r0 = a0;
+    r1 = a1;
+}
+
+// (a0 b0, a1 b1, a2 b2): three independent products, no wait states
+BD void fp_mul3(Fp& r0, Fp& r1, Fp& r2, Fp a0, Fp b0, Fp a1, Fp b1, Fp a2, Fp b2) {
+    HBG_FP_COUNT_CALL(0);
+    HBG_FP_COUNT_CALL(0);
+    HBG_FP_COUNT_CALL(0);
+    asm(HBG_FP_SUB_CALL("hbg_fpmul3")
+        : "+{v[0:11]}"(a0), "+{v[24:35]}"(a1), "+{v[48:59]}"(a2)
+        : "{v[12:23]}"(b0), "{v[36:47]}"(b1), "{v[60:71]}"(b2)
+        : HBG_FP_SUB3_CLOBBERS);
+    r0 = a0;
+    r1 = a1;
+    r2 = a2;
 }
 
 BD Fp fp_add(const Fp& a, const Fp& b) {
@@ -166,7 +183,7 @@ BD bool fp_raw_lt_p(const Fp& a) {
 // the exponent is wave-uniform, so every branch below is uniform; 8 table
 // multiplications + ~nbits/5 window multiplications instead of ~nbits/2
 // (Fermat inverse: 380 squarings + 83 multiplications instead of + 190).
-__device__ __noinline__ Fp fp_pow(Fp a, const uint32_t* __restrict__ e, int nbits) {
+BD Fp fp_pow(Fp a, const uint32_t* __restrict__ e, int nbits) {
     Fp tbl[8];
     tbl[0] = a;
     const Fp a2 = fp_sqr(a);
@@ -262,19 +279,24 @@ BD bool fp2_is_zero(const Fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1);
 BD bool fp2_eq(const Fp2& a, const Fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
 BD Fp2 fp2_select(bool c, const Fp2& a, const Fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
 
+// Karatsuba: the three products are independent -> one hbg_fpmul3 call
 BD Fp2 fp2_mul(const Fp2& a, const Fp2& b) {
-    const Fp t0 = fp_mul(a.c0, b.c0);
-    const Fp t1 = fp_mul(a.c1, b.c1);
-    const Fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+    Fp t0, t1, t2;
+    fp_mul3(t0, t1, t2, a.c0, b.c0, a.c1, b.c1, fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
     return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
 BD Fp2 fp2_sqr(const Fp2& a) {
-    const Fp t = fp_mul(a.c0, a.c1);
-    return {fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+    Fp t, u;
+    fp_mul2(t, u, a.c0, a.c1, fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+    return {u, fp_dbl(t)};
 }
 
-BD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) { return {fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+BD Fp2 fp2_mul_fp(const Fp2& a, const Fp& s) {
+    Fp r0, r1;
+    fp_mul2(r0, r1, a.c0, s, a.c1, s);
+    return {r0, r1};
+}
 
 // * (1 + u)
 BD Fp2 fp2_mul_xi(const Fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
@@ -296,7 +318,7 @@ BD bool fp2_gt(const Fp2& a, const Fp2& b) {
     return fp_gt(a.c0, b.c0);
 }
 
-__device__ __noinline__ void fp2_pow_inplace(Fp2* x, const uint32_t* __restrict__ e, int nbits) {
+BD void fp2_pow_inplace(Fp2* x, const uint32_t* __restrict__ e, int nbits) {
     const Fp2 a = *x;
     Fp2 r = a;
     for (int i = nbits - 2; i >= 0; --i) {
@@ -374,15 +396,6 @@ BD Fp6 fp6_mul_by_1(const Fp6& a, const Fp2& b1) {
     return {fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
 }
 
-// Non-inlined, pointer-passing forms of the heavy tower ops.  Operands travel
-// through private memory so each function is register-allocated on its own
-// (inlining the whole tower into one kernel needs ~460 live registers).
-__device__ __noinline__ void fp6_mul_p(Fp6* r, const Fp6* a, const Fp6* b) { *r = fp6_mul(*a, *b); }
-__device__ __noinline__ void fp6_mul_by_01_p(Fp6* r, const Fp6* a, const Fp2* b0, const Fp2* b1) {
-    *r = fp6_mul_by_01(*a, *b0, *b1);
-}
-__device__ __noinline__ void fp6_mul_by_1_p(Fp6* r, const Fp6* a, const Fp2* b1) { *r = fp6_mul_by_1(*a, *b1); }
-
 BD Fp6 fp6_inv(const Fp6& a) {
     const Fp2 c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
     const Fp2 c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
@@ -403,6 +416,15 @@ BD Fp6 fp6_frob(const Fp6& a) {
 }
 
 // ============================================================== Fp12 = Fp6[w]/(w^2 - v)
+// Register-resident: every Fp12 operation below is inlined down to the
+// fp_mul / fp_sqr calls, so its operands and temporaries live in registers
+// (the pairing kernels run one wave per SIMD: 256 VGPRs + 256 AGPRs, and
+// fp_mul clobbers only v0-v39).  Round 3's pointer-passing Fp6 / Fp12 call
+// frames round-tripped 288-576 B operands through scratch on every call
+// (295 KB of HBM traffic per verified share, profiles/r03al).  Pointers remain
+// only at the final exponentiation's Fp12 level (final_exponentiation), where
+// five values are live at once and one load / store per Fp12 operation is
+// noise next to its 18-54 multiplications.
 struct Fp12 {
     Fp6 c0, c1;
 };
@@ -411,63 +433,47 @@ BD Fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
 BD Fp12 fp12_conj(const Fp12& a) { return {a.c0, fp6_neg(a.c1)}; }
 BD bool fp12_eq(const Fp12& a, const Fp12& b) { return fp6_eq(a.c0, b.c0) && fp6_eq(a.c1, b.c1); }
 BD bool fp12_is_one(const Fp12& a) { return fp12_eq(a, fp12_one()); }
+BD Fp12 fp12_select(bool c, const Fp12& a, const Fp12& b) {
+    return {{fp2_select(c, a.c0.c0, b.c0.c0), fp2_select(c, a.c0.c1, b.c0.c1), fp2_select(c, a.c0.c2, b.c0.c2)},
+            {fp2_select(c, a.c1.c0, b.c1.c0), fp2_select(c, a.c1.c1, b.c1.c1), fp2_select(c, a.c1.c2, b.c1.c2)}};
+}
 
-__device__ __noinline__ void fp12_mul_p(Fp12* r, const Fp12* a, const Fp12* b) {
-    Fp6 t0, t1, t2, s0, s1;
-    fp6_mul_p(&t0, &a->c0, &b->c0);
-    fp6_mul_p(&t1, &a->c1, &b->c1);
-    s0 = fp6_add(a->c0, a->c1);
-    s1 = fp6_add(b->c0, b->c1);
-    fp6_mul_p(&t2, &s0, &s1);
-    r->c1 = fp6_sub(t2, fp6_add(t0, t1));
-    r->c0 = fp6_add(t0, fp6_mul_by_v(t1));
+BD Fp12 fp12_mul_v(const Fp12& a, const Fp12& b) {
+    const Fp6 t0 = fp6_mul(a.c0, b.c0);
+    const Fp6 t1 = fp6_mul(a.c1, b.c1);
+    const Fp6 t2 = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1));
+    return {fp6_add(t0, fp6_mul_by_v(t1)), fp6_sub(t2, fp6_add(t0, t1))};
 }
 
 // the crate's Fq12::square (complex squaring, 2 Fq6 mults)
-__device__ __noinline__ void fp12_sqr_p(Fp12* r, const Fp12* a) {
-    Fp6 ab, c0, c0c1;
-    fp6_mul_p(&ab, &a->c0, &a->c1);
-    c0c1 = fp6_add(a->c0, a->c1);
-    c0 = fp6_add(fp6_mul_by_v(a->c1), a->c0);
-    fp6_mul_p(&c0, &c0, &c0c1);
-    c0 = fp6_sub(c0, ab);
-    r->c1 = fp6_add(ab, ab);
-    r->c0 = fp6_sub(c0, fp6_mul_by_v(ab));
+BD Fp12 fp12_sqr_v(const Fp12& a) {
+    const Fp6 ab = fp6_mul(a.c0, a.c1);
+    const Fp6 c0 = fp6_sub(fp6_mul(fp6_add(fp6_mul_by_v(a.c1), a.c0), fp6_add(a.c0, a.c1)), ab);
+    return {fp6_sub(c0, fp6_mul_by_v(ab)), fp6_add(ab, ab)};
 }
 
-__device__ __noinline__ void fp12_inv_p(Fp12* r, const Fp12* a) {
-    Fp6 t0, t1, t;
-    fp6_mul_p(&t0, &a->c0, &a->c0);
-    fp6_mul_p(&t1, &a->c1, &a->c1);
-    t = fp6_inv(fp6_sub(t0, fp6_mul_by_v(t1)));
-    Fp6 c0, c1;
-    fp6_mul_p(&c0, &a->c0, &t);
-    fp6_mul_p(&c1, &a->c1, &t);
-    r->c0 = c0;
-    r->c1 = fp6_neg(c1);
+// f * (c0 + c1 v + c4 v w)   (the crate's Fq12::mul_by_014), in place
+BD void fp12_mul_by_014_v(Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
+    const Fp6 t = fp6_mul_by_01(fp6_add(f.c1, f.c0), c0, fp2_add(c1, c4));
+    const Fp6 aa = fp6_mul_by_01(f.c0, c0, c1);
+    const Fp6 bb = fp6_mul_by_1(f.c1, c4);
+    f.c1 = fp6_sub(fp6_sub(t, aa), bb);
+    f.c0 = fp6_add(fp6_mul_by_v(bb), aa);
+}
+
+BD Fp12 fp12_inv_v(const Fp12& a) {
+    const Fp6 t = fp6_inv(fp6_sub(fp6_mul(a.c0, a.c0), fp6_mul_by_v(fp6_mul(a.c1, a.c1))));
+    return {fp6_mul(a.c0, t), fp6_neg(fp6_mul(a.c1, t))};
 }
 
 template <int K>
-__device__ __noinline__ void fp12_frob_p(Fp12* r, const Fp12* a) {
-    const Fp6 c0 = fp6_frob<K>(a->c0), c1 = fp6_frob<K>(a->c1);
+BD Fp12 fp12_frob_v(const Fp12& a) {
+    const Fp6 c0 = fp6_frob<K>(a.c0), c1 = fp6_frob<K>(a.c1);
     Fp2 g;
     if constexpr (K == 1) g = fp2_const(kFrob12c1_1);
     if constexpr (K == 2) g = fp2_const(kFrob12c1_2);
     if constexpr (K == 3) g = fp2_const(kFrob12c1_3);
-    r->c0 = c0;
-    r->c1 = {fp2_mul(c1.c0, g), fp2_mul(c1.c1, g), fp2_mul(c1.c2, g)};
-}
-
-// f * (c0 + c1 v + c4 v w)   (the crate's Fq12::mul_by_014)
-__device__ __noinline__ void fp12_mul_by_014_p(Fp12* f, const Fp2* c0, const Fp2* c1, const Fp2* c4) {
-    Fp6 aa, bb, t;
-    fp6_mul_by_01_p(&aa, &f->c0, c0, c1);
-    fp6_mul_by_1_p(&bb, &f->c1, c4);
-    const Fp2 o = fp2_add(*c1, *c4);
-    t = fp6_add(f->c1, f->c0);
-    fp6_mul_by_01_p(&t, &t, c0, &o);
-    f->c1 = fp6_sub(fp6_sub(t, aa), bb);
-    f->c0 = fp6_add(fp6_mul_by_v(bb), aa);
+    return {c0, {fp2_mul(c1.c0, g), fp2_mul(c1.c1, g), fp2_mul(c1.c2, g)}};
 }
 
 // Granger-Scott cyclotomic squaring (valid after the easy part of the final
@@ -495,16 +501,32 @@ BD Fp12 fp12_cyclotomic_sqr_v(const Fp12& f) {
     return {{z0, z4, z3}, {z2, z1, z5}};
 }
 
-__device__ __noinline__ void fp12_cyc_sqr_p(Fp12* r, const Fp12* f) { *r = fp12_cyclotomic_sqr_v(*f); }
+// Final-exponentiation steps: one Fp12 load / store at the call boundary, the
+// body register-resident.
+__device__ __noinline__ void fp12_mul_n(Fp12* r, const Fp12* a, const Fp12* b) { *r = fp12_mul_v(*a, *b); }
+__device__ __noinline__ void fp12_inv_n(Fp12* r, const Fp12* a) { *r = fp12_inv_v(*a); }
+template <int K>
+__device__ __noinline__ void fp12_frob_n(Fp12* r, const Fp12* a) { *r = fp12_frob_v<K>(*a); }
+__device__ __noinline__ void fp12_cyc_sqr_n(Fp12* r, const Fp12* a) { *r = fp12_cyclotomic_sqr_v(*a); }
 
 // *f = conj(f^e) for a 64-bit e with top set bit `top` (cyclotomic squarings);
-// with e = |x| this is the crate's exp_by_x (x < 0).
+// with e = |x| this is the crate's exp_by_x (x < 0).  Square-and-multiply
+// split into runs: the inner loop squares down to the next set bit with only
+// the accumulator live (|x| has 5 set bits below its top, so the base is
+// touched 5 times in 63 steps and waits outside the loop).
 __device__ __noinline__ void fp12_cyc_pow_conj(Fp12* f, uint64_t e, int top) {
-    Fp12 a = *f;
+    const Fp12 a = *f;
     Fp12 r = a;
-    for (int i = top - 1; i >= 0; --i) {
-        fp12_cyc_sqr_p(&r, &r);
-        if ((e >> i) & 1ull) fp12_mul_p(&r, &r, &a);
+    uint64_t rem = e & ((1ull << top) - 1ull);
+    int i = top - 1;
+#pragma unroll 1
+    for (;;) {
+        const int nb = rem ? 63 - __builtin_clzll(rem) : -1;  // next set bit (wave-uniform)
+#pragma unroll 1
+        for (; i >= (nb < 0 ? 0 : nb); --i) r = fp12_cyclotomic_sqr_v(r);
+        if (nb < 0) break;
+        r = fp12_mul_v(r, a);
+        rem &= ~(1ull << nb);
     }
     *f = fp12_conj(r);
 }
@@ -683,6 +705,10 @@ BD G2 g2_dbl_v(const G2& p) {
     return r;
 }
 
+// G2 point steps stay out of line (one call per step of a scalar
+// multiplication / G2Prepared: keeps the G2 kernels' code and compile time
+// bounded).  Only one-wave-per-SIMD kernels call them (TDEC_WAVE1_KERNEL), so
+// every caller shares their 512-register budget.
 __device__ __noinline__ void g2_dbl_p(G2* r, const G2* p) { *r = g2_dbl_v(*p); }
 BD G2 g2_dbl(const G2& p) {
     G2 r;
@@ -859,47 +885,47 @@ BD LineCoeff g2_addition_step(G2& r, const Fp2& qx, const Fp2& qy) {
 // bit of |x|>>1 ... (bits of |x|>>1 below its top bit) + additions + final doubling
 constexpr int kMillerSteps = 68;
 
-// ell(f, coeffs, p) of the crate, in place
-BD void ell(Fp12* f, const LineCoeff& c, const Fp& px, const Fp& py) {
-    const Fp2 c1 = fp2_mul_fp(c.c1, px), c4 = fp2_mul_fp(c.c0, py);
-    fp12_mul_by_014_p(f, &c.c2, &c1, &c4);
+// ell(f, coeffs, p) of the crate, in place: the line evaluated at affine
+// P = (px, py) times the sparse Fp12 (c2, c1 px, c0 py) -> mul_by_014
+BD void ell(Fp12& f, const LineCoeff& c, const Fp& px, const Fp& py) {
+    fp12_mul_by_014_v(f, c.c2, fp2_mul_fp(c.c1, px), fp2_mul_fp(c.c0, py));
 }
 
 // the crate's final_exponentiation, in place
 __device__ __noinline__ void final_exponentiation(Fp12* io) {
-    Fp12 r, f1, f2, y0, y1, y2, y3;
-    f1 = fp12_conj(*io);
-    fp12_inv_p(&f2, io);
-    fp12_mul_p(&r, &f1, &f2);
+    Fp12 r, f2, y0, y1, y2, y3;
+    fp12_inv_n(&f2, io);
+    y3 = fp12_conj(*io);
+    fp12_mul_n(&r, &y3, &f2);
     f2 = r;
-    fp12_frob_p<2>(&r, &r);
-    fp12_mul_p(&r, &r, &f2);
-    fp12_cyc_sqr_p(&y0, &r);
+    fp12_frob_n<2>(&r, &r);
+    fp12_mul_n(&r, &r, &f2);
+    fp12_cyc_sqr_n(&y0, &r);
     y1 = y0;
     fp12_exp_by_x_inplace(&y1);
     y2 = y1;
     fp12_cyc_pow_conj(&y2, kBlsX >> 1, 62);  // conj(y1^(|x|>>1))
     y3 = fp12_conj(r);
-    fp12_mul_p(&y1, &y1, &y3);
+    fp12_mul_n(&y1, &y1, &y3);
     y1 = fp12_conj(y1);
-    fp12_mul_p(&y1, &y1, &y2);
+    fp12_mul_n(&y1, &y1, &y2);
     y2 = y1;
     fp12_exp_by_x_inplace(&y2);
     y3 = y2;
     fp12_exp_by_x_inplace(&y3);
     y1 = fp12_conj(y1);
-    fp12_mul_p(&y3, &y3, &y1);
+    fp12_mul_n(&y3, &y3, &y1);
     y1 = fp12_conj(y1);
-    fp12_frob_p<3>(&y1, &y1);
-    fp12_frob_p<2>(&y2, &y2);
-    fp12_mul_p(&y1, &y1, &y2);
+    fp12_frob_n<3>(&y1, &y1);
+    fp12_frob_n<2>(&y2, &y2);
+    fp12_mul_n(&y1, &y1, &y2);
     y2 = y3;
     fp12_exp_by_x_inplace(&y2);
-    fp12_mul_p(&y2, &y2, &y0);
-    fp12_mul_p(&y2, &y2, &r);
-    fp12_mul_p(&y1, &y1, &y2);
-    fp12_frob_p<1>(&y2, &y3);
-    fp12_mul_p(io, &y1, &y2);
+    fp12_mul_n(&y2, &y2, &y0);
+    fp12_mul_n(&y2, &y2, &r);
+    fp12_mul_n(&y1, &y1, &y2);
+    fp12_frob_n<1>(&y2, &y3);
+    fp12_mul_n(io, &y1, &y2);
 }
 
 #undef BD

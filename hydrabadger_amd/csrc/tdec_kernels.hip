@@ -39,6 +39,13 @@ namespace bls {
 #define HBG_TDEC_WPE 2
 #endif
 #define TDEC_KERNEL __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HBG_TDEC_WPE)))
+// Pairing and G2 kernels (a Miller loop + final exponentiation, or G2 point
+// arithmetic, per lane): one wave per SIMD in both builds.  The
+// register-resident Fp12 tower (bls.h) keeps a line evaluation's ~450 live
+// values in the 256 VGPRs + 256 AGPRs a lone wave owns, and Fp2 products are
+// three interleaved Montgomery chains (hbg_fpmul3), so a lone wave still
+// issues back to back.  G1-only kernels stay at HBG_TDEC_WPE.
+#define TDEC_WAVE1_KERNEL __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 
 #define BD __device__ __forceinline__
 
@@ -162,8 +169,9 @@ struct ChaChaRng {
 // ------------------------------------------------------------------ long messages (a13, a16)
 // xor_with_hash's keystream and hash_g1_g2's SHA3(V) for contributions of any
 // length (in HoneyBadger V is the whole serialised contribution):
-//  * the keystream is seekable by block counter: one 256-thread block per
-//    item, threads over its ChaCha20 blocks; block c covers output bytes
+//  * the keystream is seekable by block counter: a 256-thread workgroup per
+//    item (items strided over a capped grid, so the item count sets no grid
+//    limit), threads over its ChaCha20 blocks; block c covers output bytes
 //    [16c, 16c + 16) (rand's `Standard` u8 is the low byte of each next_u32);
 //  * SHA3(V) reads V a dword at a time (aligned loads + v_alignbyte) into the
 //    bank-allocated Keccak round (keccak_asm.h), one lane per item.
@@ -172,8 +180,8 @@ __global__ __launch_bounds__(256) void tdec_keystream_xor(uint64_t n, const uint
                                                           const uint8_t* __restrict__ in,
                                                           const uint64_t* __restrict__ off, uint8_t* __restrict__ out,
                                                           const int32_t* __restrict__ status) {
-    const uint64_t k = blockIdx.x;
-    if (k >= n || (status && status[k] != 0)) return;  // no output for a failed item (its bytes stay untouched)
+    for (uint64_t k = blockIdx.x; k < n; k += gridDim.x) {
+    if (status && status[k] != 0) continue;  // no output for a failed item (its bytes stay untouched)
     uint32_t key[8];
     const uint8_t* sd = seeds + 32 * k;
 #pragma unroll
@@ -189,6 +197,7 @@ __global__ __launch_bounds__(256) void tdec_keystream_xor(uint64_t n, const uint
 #pragma unroll
         for (int b = 0; b < 16; ++b)
             if (b0 + b < len) out[o + b0 + b] = in[o + b0 + b] ^ (uint8_t)(w[b] & 0xFFu);
+    }
     }
 }
 
@@ -601,77 +610,80 @@ BD void g2_prepare(const Fp2& qx, const Fp2& qy, uint32_t* out) {
     store_line(out + 72 * k, g2_doubling_step(r));
 }
 
-// Miller loop over two pairs with prepared lines (the crate's miller_loop);
-// a pair is skipped when its G1 or G2 point is the identity.
-__device__ __noinline__ void miller_loop2(Fp12* out, const uint32_t* c1, Fp p1x, Fp p1y, bool use1,
-                                          const uint32_t* c2, Fp p2x, Fp p2y, bool use2) {
-    Fp12 f = fp12_one();
+// Miller loop over two pairs with prepared lines (the crate's miller_loop),
+// register-resident (bls.h: the Fp12 tower inlined down to fp_mul / fp_sqr).
+// The crate's order — for each bit i = 61..0 of |x|>>1 below its top: the
+// doubling line, the addition line when the bit is set, then f^2; last the
+// final doubling line — is flattened into one loop over the 68 lines with
+// "f^2 after line k" from a constant schedule, and the two pairs into an
+// inner loop, so the kernel holds ONE inlined line evaluation and ONE
+// squaring (code size: the body is ~80 multiplication call sites).  A pair is
+// skipped when its G1 or G2 point is the identity.
+struct MillerSched {
+    uint32_t w[3];
+};
+constexpr MillerSched miller_sched() {
+    MillerSched s{{0u, 0u, 0u}};
     int k = 0;
     for (int i = 61; i >= 0; --i) {
-        if (use1) ell(&f, load_line(c1 + 72 * k), p1x, p1y);
-        if (use2) ell(&f, load_line(c2 + 72 * k), p2x, p2y);
-        ++k;
-        if ((kXHalf >> i) & 1ull) {
-            if (use1) ell(&f, load_line(c1 + 72 * k), p1x, p1y);
-            if (use2) ell(&f, load_line(c2 + 72 * k), p2x, p2y);
-            ++k;
-        }
-        fp12_sqr_p(&f, &f);
+        ++k;                              // doubling line
+        if ((kXHalf >> i) & 1ull) ++k;    // addition line
+        s.w[(k - 1) >> 5] |= 1u << ((k - 1) & 31);  // f^2 after line k - 1
     }
-    if (use1) ell(&f, load_line(c1 + 72 * k), p1x, p1y);
-    if (use2) ell(&f, load_line(c2 + 72 * k), p2x, p2y);
-    *out = fp12_conj(f);
+    return s;
+}
+constexpr MillerSched kMillerSqr = miller_sched();
+static_assert(kMillerSqr.w[2] >> 3 == 0, "68 lines: f^2 never follows the last one");
+
+// JAC: pair j's G1 point is Jacobian (X, Y, Z), passed as (a, b, z) =
+// (XZ, Y, Z^3): each line value at (X/Z^2, Y/Z^3) is taken times Z^3
+// (c2 Z^3 + c1 XZ + c0 Y), an Fp factor that the final exponentiation maps
+// to 1 ((p - 1) divides (p^12 - 1) / r) — no inversion for a conversion to
+// affine.  Otherwise (a, b) = affine (x, y) and z is unused.
+template <bool JAC>
+BD Fp12 miller_loop2(const uint32_t* c1, const Fp& a1, const Fp& b1, const Fp& z1, bool use1, const uint32_t* c2,
+                     const Fp& a2, const Fp& b2, const Fp& z2, bool use2) {
+    Fp12 f = fp12_one();
+#pragma unroll 1
+    for (int k = 0; k < kMillerSteps; ++k) {
+#pragma unroll 1
+        for (int j = 0; j < 2; ++j) {
+            if (j ? use2 : use1) {
+                const LineCoeff c = load_line((j ? c2 : c1) + 72 * k);
+                const Fp a = j ? a2 : a1, b = j ? b2 : b1;
+                if constexpr (JAC) {
+                    const Fp z = j ? z2 : z1;
+                    fp12_mul_by_014_v(f, fp2_mul_fp(c.c2, z), fp2_mul_fp(c.c1, a), fp2_mul_fp(c.c0, b));
+                } else {
+                    ell(f, c, a, b);
+                }
+            }
+        }
+        if ((kMillerSqr.w[k >> 5] >> (k & 31)) & 1u) f = fp12_sqr_v(f);
+    }
+    return fp12_conj(f);
 }
 
 // one pairing check: prod e(P_i, Q_i) == 1 over the two prepared pairs
 BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool use1, const uint32_t* c2,
                        const Fp& p2x, const Fp& p2y, bool use2) {
-    Fp12 f;
-    miller_loop2(&f, c1, p1x, p1y, use1, c2, p2x, p2y, use2);
+    Fp12 f = miller_loop2<false>(c1, p1x, p1y, p1y, use1, c2, p2x, p2y, p2y, use2);
     final_exponentiation(&f);
     return fp12_is_one(f);
 }
 
-// The same check for Jacobian G1 points P = (X, Y, Z), Z != 0, without the two
-// inversions of a conversion to affine: each line value at (X/Z^2, Y/Z^3) is
-// taken times Z^3 (c2 Z^3 + c1 XZ + c0 Y), an Fp factor that the final
-// exponentiation maps to 1 ((p - 1) divides (p^12 - 1) / r).  Inputs: XZ, Y, Z^3.
-BD void ell_jac(Fp12* f, const LineCoeff& c, const Fp& xz, const Fp& y, const Fp& z3) {
-    const Fp2 c0 = fp2_mul_fp(c.c2, z3), c1 = fp2_mul_fp(c.c1, xz), c4 = fp2_mul_fp(c.c0, y);
-    fp12_mul_by_014_p(f, &c0, &c1, &c4);
-}
-__device__ __noinline__ void miller_loop2_jac(Fp12* out, const uint32_t* c1, Fp p1xz, Fp p1y, Fp p1z3, bool use1,
-                                              const uint32_t* c2, Fp p2xz, Fp p2y, Fp p2z3, bool use2) {
-    Fp12 f = fp12_one();
-    int k = 0;
-    for (int i = 61; i >= 0; --i) {
-        if (use1) ell_jac(&f, load_line(c1 + 72 * k), p1xz, p1y, p1z3);
-        if (use2) ell_jac(&f, load_line(c2 + 72 * k), p2xz, p2y, p2z3);
-        ++k;
-        if ((kXHalf >> i) & 1ull) {
-            if (use1) ell_jac(&f, load_line(c1 + 72 * k), p1xz, p1y, p1z3);
-            if (use2) ell_jac(&f, load_line(c2 + 72 * k), p2xz, p2y, p2z3);
-            ++k;
-        }
-        fp12_sqr_p(&f, &f);
-    }
-    if (use1) ell_jac(&f, load_line(c1 + 72 * k), p1xz, p1y, p1z3);
-    if (use2) ell_jac(&f, load_line(c2 + 72 * k), p2xz, p2y, p2z3);
-    *out = fp12_conj(f);
-}
 // e(P1, Q1) e(P2, Q2) == 1 for Jacobian P1, P2 (an identity point: its pair is skipped)
 BD bool pairing_check2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2, const G1& p2, bool use2) {
     const bool u1 = !fp_is_zero(p1.z), u2 = use2 && !fp_is_zero(p2.z);
     const Fp z1 = fp_sqr(p1.z), z2 = fp_sqr(p2.z);
-    Fp12 f;
-    miller_loop2_jac(&f, c1, fp_mul(p1.x, p1.z), p1.y, fp_mul(z1, p1.z), u1, c2, fp_mul(p2.x, p2.z), p2.y,
-                     fp_mul(z2, p2.z), u2);
+    Fp12 f = miller_loop2<true>(c1, fp_mul(p1.x, p1.z), p1.y, fp_mul(z1, p1.z), u1, c2, fp_mul(p2.x, p2.z), p2.y,
+                                fp_mul(z2, p2.z), u2);
     final_exponentiation(&f);
     return fp12_is_one(f);
 }
 
 // ------------------------------------------------------------------ kernels
-TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
+TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
                                                       const uint8_t* __restrict__ V,
                                                       const uint64_t* __restrict__ V_off,
                                                       const uint8_t* __restrict__ vdig,
@@ -703,7 +715,7 @@ TDEC_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
 // The W half of ciphertext preparation (decode + subgroup check + the
 // G2Prepared lines of W): independent of V, so it runs on a second stream
 // while SHA3(V) and hash_g1_g2 run (stage_ct in api.hip).
-TDEC_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
+TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
                                    int32_t* __restrict__ w_status, uint32_t* __restrict__ coefW) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -733,7 +745,7 @@ TDEC_KERNEL void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
     pk_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
 }
 
-TDEC_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restrict__ n_dev,
+TDEC_WAVE1_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restrict__ n_dev,
                                                          const uint8_t* __restrict__ share48,
                                                          const uint32_t* __restrict__ share_ct,
                                                          const uint32_t* __restrict__ share_pk,
@@ -1043,7 +1055,7 @@ BD void batch_tree_step(bool pass, const CheckItem& it, const BatchDesc& d, cons
 // the list `items` (count *n_dev) or, with items == null, every batch
 // (count *n_dev = the batch count); the grid covers `cap` items, lanes past
 // the device count return at once.
-TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, const CheckItem* __restrict__ items,
+TDEC_WAVE1_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, const CheckItem* __restrict__ items,
                                                        const BatchDesc* __restrict__ desc,
                                                        const uint32_t* __restrict__ perm,
                                                        const uint32_t* __restrict__ sums,
@@ -1077,7 +1089,7 @@ TDEC_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_d
     batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n);
 }
 
-TDEC_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
+TDEC_WAVE1_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
                                                      const int32_t* __restrict__ ct_status,
                                                      const uint32_t* __restrict__ coefH,
                                                      const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok) {
@@ -1638,7 +1650,7 @@ BD G2A hash_g2_msg(const uint8_t* msg, uint32_t len) {
 }
 
 // SecretKey::sign(msg) = hash_g2(msg) * sk
-TDEC_KERNEL void bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* __restrict__ sk32,
+TDEC_WAVE1_KERNEL void bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* __restrict__ sk32,
                           const uint32_t* __restrict__ msg_sk, const uint8_t* __restrict__ msg,
                           const uint64_t* __restrict__ off, uint8_t* __restrict__ sig96, int32_t* __restrict__ err) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1658,7 +1670,7 @@ TDEC_KERNEL void bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* __restrict__
 
 // PublicKey::verify(sig, msg): e(pk, hash_g2(msg)) == e(G1, sig); the signature
 // decodes with the crate's subgroup check (SignedWireMessage deserialisation).
-TDEC_KERNEL void bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
+TDEC_WAVE1_KERNEL void bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
                             const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ msg_pk,
                             const uint8_t* __restrict__ msg, const uint64_t* __restrict__ off,
                             const uint8_t* __restrict__ sig96, uint32_t* __restrict__ lines, uint8_t* __restrict__ ok,
@@ -1698,7 +1710,7 @@ __device__ __forceinline__ uint64_t wire_le(const uint8_t* p, int nb) {
     return v;
 }
 
-TDEC_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_aff,
+TDEC_WAVE1_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_aff,
                                     const int32_t* __restrict__ pk_status, uint32_t n_pk,
                                     const uint32_t* __restrict__ frame_pk, const uint8_t* __restrict__ frames,
                                     const uint64_t* __restrict__ off, uint32_t* __restrict__ lines,
@@ -1774,7 +1786,7 @@ TDEC_KERNEL void tdec_encrypt_u(uint64_t n, const uint32_t* __restrict__ pk_aff,
     sha3_bytes(cg, 48, seeds + 32ull * k);
 }
 
-TDEC_KERNEL void tdec_encrypt_w(uint64_t n, const uint8_t* __restrict__ r32, const uint8_t* __restrict__ U48,
+TDEC_WAVE1_KERNEL void tdec_encrypt_w(uint64_t n, const uint8_t* __restrict__ r32, const uint8_t* __restrict__ U48,
                                 const uint8_t* __restrict__ V, const uint64_t* __restrict__ off,
                                 const uint8_t* __restrict__ vdig, const int32_t* __restrict__ est,
                                 uint8_t* __restrict__ W96) {
@@ -1841,7 +1853,7 @@ BD G2 g2_shfl_xor(const G2& p, int m) {
 }
 
 template <int G>
-TDEC_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share96,
+TDEC_WAVE1_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* __restrict__ share96,
                                   const uint32_t* __restrict__ idx, uint8_t* __restrict__ sig96,
                                   uint8_t* __restrict__ parity, int32_t* __restrict__ status) {
     static_assert(G == 32 || G == 64, "group = half or whole wave");
@@ -1927,7 +1939,7 @@ BD G2 load_g2jac(const uint32_t* d) {
 }
 
 // per document: seed = SHA3-256(doc) (the ChaCha seed of hash_g2), G2Prepared lines of H
-TDEC_KERNEL void sig_doc_prepare(uint32_t n, const uint8_t* __restrict__ doc, const uint64_t* __restrict__ off,
+TDEC_WAVE1_KERNEL void sig_doc_prepare(uint32_t n, const uint8_t* __restrict__ doc, const uint64_t* __restrict__ off,
                                  uint32_t* __restrict__ coefH, uint8_t* __restrict__ seeds) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -1964,7 +1976,7 @@ BD G2 g2_mul_ab32(const Fp2& px, const Fp2& py, uint32_t a, uint32_t b) {
     return r;
 }
 
-TDEC_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_doc,
+TDEC_WAVE1_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_doc,
                                   const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                   const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_pk,
                                   const uint8_t* __restrict__ seeds, const uint32_t* __restrict__ pk_aff,
@@ -2061,7 +2073,7 @@ BD bool sig_pair_check(const uint32_t* coefH, const Fp& pkx, const Fp& pky, bool
 // batch, or with `spec` over every batch AND its four 16-groups, item
 // 5b + j, so a small batch count does not pay a separate latency-bound round
 // for the 16-groups); lines: one G2Prepared slot per lane of this launch.
-TDEC_KERNEL void sig_batch_check(uint64_t base, uint32_t cap, const uint32_t* __restrict__ n_dev, uint32_t spec,
+TDEC_WAVE1_KERNEL void sig_batch_check(uint64_t base, uint32_t cap, const uint32_t* __restrict__ n_dev, uint32_t spec,
                                  const CheckItem* __restrict__ items,
                                  const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                  const uint32_t* __restrict__ sums, const uint8_t* __restrict__ leaf_ok,
@@ -2092,7 +2104,7 @@ TDEC_KERNEL void sig_batch_check(uint64_t base, uint32_t cap, const uint32_t* __
 
 // Per-share PublicKeyShare::verify with H prepared per document: share
 // sel[base + i] (or base + i), lines: one G2Prepared slot per lane.
-TDEC_KERNEL void sig_verify_shares(uint64_t base, uint64_t cap, const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ sel,
+TDEC_WAVE1_KERNEL void sig_verify_shares(uint64_t base, uint64_t cap, const uint32_t* __restrict__ n_dev, const uint32_t* __restrict__ sel,
                                    const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_doc,
                                    const uint32_t* __restrict__ share_pk, const uint32_t* __restrict__ pk_aff,
                                    const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ coefH,
@@ -2117,7 +2129,7 @@ TDEC_KERNEL void sig_verify_shares(uint64_t base, uint64_t cap, const uint32_t* 
 //     5 pairing(P,Q) = final_exp(miller)  6 hash_g2(seed)  7 miller_loop(P,Q) 8 final_exp(f)
 //     9 [k]P (64-bit k)  10 P + Q (Jacobian add)  11 Legendre(a), is_square(a + b u)
 // Field values cross the boundary as canonical raw limbs (12 u32 LE).
-TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
+TDEC_WAVE1_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
                                                 uint32_t* __restrict__ out, uint32_t in_words,
                                                 uint32_t out_words, uint32_t* __restrict__ lines) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2161,8 +2173,7 @@ TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
         // in: P.x P.y Q.x0 Q.x1 Q.y0 Q.y1 (canonical affine)
         uint32_t* ln = lines + (uint64_t)k * 72 * kMillerSteps;
         g2_prepare({ld(24), ld(36)}, {ld(48), ld(60)}, ln);
-        Fp12 f;
-        miller_loop2(&f, ln, ld(0), ld(12), true, ln, ld(0), ld(12), false);
+        Fp12 f = miller_loop2<false>(ln, ld(0), ld(12), ld(12), true, ln, ld(0), ld(12), ld(12), false);
         if (op == 5) final_exponentiation(&f);
         st12(f);
     } else if (op == 6) {
@@ -2201,13 +2212,12 @@ TDEC_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict__ in,
 
 // ------------------------------------------------------------------ launchers
 // Latency build: tdec_kernels_lat.hip compiles this file a second time into
-// namespace bls_lat with HBG_FP_LAT (three interleaved accumulators per Fp
-// multiplication column, bls_fp_mul.h) and one wave per SIMD's register
-// budget.  Launches of at most g_lat_lanes lanes (one wave per SIMD: the
+// namespace bls_lat with a one-wave-per-SIMD register budget for every
+// kernel.  Launches of at most g_lat_lanes lanes (one wave per SIMD: the
 // epoch's 128 ciphertexts, up to ~65 k messages) take those kernels — a lone
-// wave's multiplication is a dependency chain, and its scratch round trips
-// are what a larger register budget removes — and larger ones the serial
-// chain at two waves per SIMD, which issues fewer instructions.
+// wave has the whole register file and its Fp2 products run as three
+// interleaved chains (hbg_fpmul3) — and larger ones the G1 kernels at two
+// waves per SIMD.
 #if HBG_TDEC_LAT_TU || defined(HBG_FP_COUNT) || defined(HBG_DEBUG_CHECKS)
 // (the latency build itself, and the instrumented / diagnostic tool builds:
 // every launch stays in this build so counts and checks see all of it)
@@ -2308,8 +2318,9 @@ hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uin
                                      uint8_t* out, const int32_t* status, hipStream_t st) {
     HBG_COUNT_MARK("tdec_keystream_xor", st);
     if (n == 0) return hipSuccess;
-    HBG_GRID_CHECK(n, 256);
-    tdec_keystream_xor<<<dim3((uint32_t)n), dim3(256), 0, st>>>(n, seeds, in, off, out, status);
+    constexpr uint64_t kMaxBlocks = 1ull << 16;  // items stride over the grid beyond this
+    tdec_keystream_xor<<<dim3((uint32_t)(n < kMaxBlocks ? n : kMaxBlocks)), dim3(256), 0, st>>>(n, seeds, in, off,
+                                                                                             out, status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
@@ -2495,6 +2506,7 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
     HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 32 ? 32u : 64u), launch_tdec_combine(n, t, share48, idx, V, V_off, out, status, scratch, seeds, st));
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK(n, 64);  // every grid of this call, before the first launch
     if (t + 1 <= 32)
         tdec_combine_msm<32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
     else if (t + 1 <= 64)
@@ -2540,6 +2552,7 @@ hipError_t launch_tdec_encrypt(uint64_t n, const uint32_t* pk_aff, const int32_t
     HBG_LAT_DISPATCH(n, launch_tdec_encrypt(n, pk_aff, pk_status, r32, msg, off, U48, V, W96, seeds, vdig, est, err, st));
     HBG_COUNT_MARK("tdec_encrypt", st);
     if (n == 0) return hipSuccess;
+    HBG_GRID_CHECK((n + 63) / 64, 64);  // every grid of this call (v_digest's too), before the first launch
     tdec_encrypt_u<<<grid64(n), dim3(64), 0, st>>>(n, pk_aff, pk_status, r32, U48, W96, seeds, est, err);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = launch_tdec_keystream_xor(n, seeds, msg, off, V, est, st);

@@ -18,26 +18,39 @@ step message to its peers at handler.rs:747-764).  Per epoch:
    bytes (RCCL over xGMI); every rank parses them (``hbg_rbc_read_msgs``) and
    checks them (``hbg_merkle_validate``): node j accepts p's Value iff it
    parses, is a Value, carries index j and validates;
+   With ``per_node`` (the default) the Values travel by one all-to-all: a
+   rank receives only the messages addressed to its own nodes, and node j
+   validates its N Values (hbbft rejects a Value for another index before
+   hashing it), N*m per rank instead of N*N;
 3. Echo: each local node j sends ``Echo(proof)`` (the Value bytes, variant 1)
-   for every accepted Value — one all-gather; every Echo is parsed and
-   validated once per rank (all local nodes receive the same echoes) and
-   counted iff it carries the sender's index and validates; echoes are
-   counted per root hash;
+   for every accepted Value — one all-gather; every Echo is parsed once per
+   rank and validated by EVERY local node (``per_node``: m*N*N
+   ``Proof::validate`` per rank, the N^3 of the network spread over the
+   ranks; the shared view validates each echo once on behalf of all local
+   nodes) and counted iff it carries the sender's index and validates;
+   echoes are counted per root hash;
 4. Ready: a node sends ``Ready(root)`` (bincode, 36 B) once a root has N - f
    echoes — one all-gather, parsed and counted; an instance is delivered with
    2f + 1 Readys and N - 2f echoes for its root (all correct nodes see the
    same messages, so Ready amplification adds nothing and is not modelled);
 5. decode: ``decode_from_shards`` of every delivered instance from the echoes
-   carrying its root (``hbg_rbc_decode``);
+   carrying its root (``hbg_rbc_decode``) — by every local node (``per_node``:
+   each reconstructs its own copy, m*N decodes per rank, in chunks of nodes);
 6. Subset accepts every delivered proposal (binary agreement is out of scope)
    whose bytes parse as a ciphertext;
 7. ThresholdDecrypt: each local node's decryption share of every accepted
    ciphertext (``hbg_tdec_decrypt_shares``) — one all-gather — then
-   ``hbg_tdec_threshold_decrypt`` with a seeded arrival order per ciphertext:
-   set_ciphertext check, faults for invalid shares, the first t+1 valid
-   shares (t = f), late shares ignored.
+   ``hbg_tdec_threshold_decrypt``: with ``per_node`` every local node runs
+   its own instance of every accepted ciphertext with its own seeded arrival
+   order (m*k instances per rank: set_ciphertext / Ciphertext::verify and
+   the verification of every share it handles, at every node, as hbbft
+   does); the shared view runs one instance per ciphertext for all nodes.
+   Either way: faults for invalid shares, the first t+1 valid shares
+   (t = f), late shares ignored.
 
-Every rank ends with the same epoch result.  The work is in an ``engine``:
+The RBC outcomes are the same at every node under full delivery; the TDec
+results come per view (``views``: this rank's node ids, or [-1] for the
+shared view).  The work is in an ``engine``:
 ``network.DeviceEngine`` (libhbgpu.so on this rank's GPU) is the product;
 tests also drive this orchestration with an oracle-backed engine under gloo
 to rehearse the exchange without a GPU, and check both against
@@ -55,7 +68,7 @@ import torch.distributed as dist
 from . import _lib
 from . import broadcast as bc
 from . import tdec_workload as tw
-from .network import all_gather_rows, proof_index_map
+from .network import all_gather_rows, all_to_all_bytes, proof_index_map
 from .workload import SplitMix64
 
 TAG_CONTRIB, TAG_R, TAG_ARRIVAL = 6, 7, 8
@@ -71,12 +84,18 @@ def instance_id(epoch: int, p: int) -> int:
     return (epoch << 20) | p
 
 
-def arrival_orders(epoch: int, proposers, n: int) -> np.ndarray:
+def arrival_id(epoch: int, p: int, node: int = -1) -> int:
+    """Seed id of an arrival order: instance p's shared view (node -1) or node `node`'s."""
+    return instance_id(epoch, p) | (0 if node < 0 else (node + 1) << 40)
+
+
+def arrival_orders(epoch: int, proposers, n: int, node: int = -1) -> np.ndarray:
     """[k][n] senders of instance proposers[k]'s decryption shares in arrival
-    order (a seeded permutation: the network's timing, an input)."""
+    order at `node` (-1: the shared view) — a seeded permutation: the
+    network's timing, an input."""
     out = np.zeros((len(proposers), n), np.int64)
     for k, p in enumerate(proposers):
-        rng = SplitMix64(TAG_ARRIVAL, instance_id(epoch, int(p)))
+        rng = SplitMix64(TAG_ARRIVAL, arrival_id(epoch, int(p), node))
         keys = [rng.next() for _ in range(n)]
         out[k] = sorted(range(n), key=lambda s: (keys[s], s))
     return out
@@ -102,11 +121,13 @@ class EpochResult:
     payloads: torch.Tensor       # [N p][C] decoded proposal bytes (rows of delivered instances)
     payload_ok: torch.Tensor     # [N p] delivered, decoded and parsed as a ciphertext
     accepted: list               # proposers of the accepted ciphertexts, ascending
-    ct_status: torch.Tensor      # [k] 0 or HBG_E_INVALID_CIPHERTEXT / HBG_E_NOT_ENOUGH_SHARES
-    plaintexts: torch.Tensor     # [k][P] (rows with status 0)
-    share_outcome: torch.Tensor  # [k][N] HBG_SHARE_*
+    views: list                  # TDec views: this rank's node ids (per node) or [-1] (shared view)
+    ct_status: torch.Tensor      # [view][k] 0 or HBG_E_INVALID_CIPHERTEXT / HBG_E_NOT_ENOUGH_SHARES
+    plaintexts: torch.Tensor     # [view][k][P] (rows with status 0)
+    share_outcome: torch.Tensor  # [view][k][N] HBG_SHARE_*
     times_ms: dict
-    exchange_bytes: int          # bytes this rank received in the epoch's all-gathers
+    exchange_bytes: int          # bytes this rank received in the epoch's collectives
+    work: dict                   # per-rank counts: Value / Echo validations, decodes, TDec instances and shares
 
 
 class HoneyBadgerEpoch:
@@ -158,12 +179,62 @@ class HoneyBadgerEpoch:
         ser[:, CT_HEAD + P:C] = W
         return ser, msgs
 
-    def run(self, epoch: int = 0, faults: Faults = Faults()) -> EpochResult:
+    def _value_round(self, vbuf, v_off, vsent, per_node: bool):
+        """Deliver the Value messages and check them at their recipients.
+        Returns (value_ok [N p][N j], the received bytes, the byte offset of
+        (source rank, local recipient a)'s run of m messages, validations)."""
+        e, N, m, L, r0 = self.engine, self.N, self.m, self.L, self.rank * self.m
+        dev = e.device
+        lens = self.msg_len
+        vsent_all = self._gather(vsent.view(1, N, m)).view(self.world, N, m)   # [r'][j][p local to r']
+        if per_node:
+            # all-to-all: rank r' sends rank r the messages (j in r's nodes, p in r')
+            rank_bytes = [m * int(lens[q * m:(q + 1) * m].sum()) for q in range(self.world)]
+            B = rank_bytes[self.rank]
+            vrecv = all_to_all_bytes(vbuf, rank_bytes, [B] * self.world, self.world, self.group)
+            self._recv += (self.world - 1) * B
+            mine = lens[r0:r0 + m]
+            g_len = np.tile(np.repeat(mine, m), self.world)   # (r', a, b): msg_len[r0 + a]
+            run_off = lambda rs, a: rs * B + m * int(mine[:a].sum())
+            j_of = torch.arange(r0, r0 + m, dtype=torch.int32, device=dev).repeat_interleave(m).repeat(self.world)
+            sent = vsent_all[:, r0:r0 + m, :]                 # [r'][a][b]
+        else:
+            vrecv = self._gather(vbuf)                        # [r'][j][p local to r']: every message
+            B = int(v_off[-1])
+            g_len = np.tile(np.repeat(lens, m), self.world)
+            run_off = lambda rs, a: rs * B + m * int(lens[:r0 + a].sum())
+            j_of = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(m).repeat(self.world)
+            sent = vsent_all
+        g_off = np.zeros(len(g_len) + 1, np.int64)
+        g_off[1:] = np.cumsum(g_len)
+        tag, vals, idx, dig, nd, roots, st = e.read_msgs(N, L, vrecv, g_off)
+        vok = e.validate_table(N, L, vals, idx, dig, nd, roots)
+        good = (st == 0) & (tag == _lib.HBG_MSG_VALUE) & (idx == j_of) & (vok == 1)
+        if per_node:
+            good = good.view(self.world, m, m) & (sent == 1)  # [r'][a][b]
+            local_ok = good.permute(0, 2, 1).reshape(N, m)    # [p][j local]
+            value_ok = self._gather(local_ok.t().contiguous().to(torch.uint8)).t().bool()   # [p][j]
+        else:
+            good = good.view(self.world, N, m) & (sent == 1)
+            value_ok = good.permute(0, 2, 1).reshape(N, N)
+        return value_ok, vrecv, run_off, len(g_len)
+
+    def run(self, epoch: int = 0, faults: Faults = Faults(), per_node: bool = True,
+            decode_chunk: int = 8) -> EpochResult:
+        """One epoch.  per_node: every local node does its own work (Values
+        addressed to it, all echoes, its decodes, its ThresholdDecrypt of every
+        accepted ciphertext with its own arrival order); otherwise the shared
+        view (one check / decode / TDec instance per rank on behalf of all
+        its nodes).  decode_chunk: local nodes whose decode copies are
+        resident at once."""
         e, N, m, L, C, P, f = self.engine, self.N, self.m, self.L, self.C, self.P, self.f
         dev = e.device
         r0 = self.rank * m
         local = self.local_nodes()
+        views = list(local) if per_node else [-1]
+        nv = len(views)
         self._recv = 0
+        work = {}
         times = {}
         t0 = time.perf_counter()
         # ---- 1. propose
@@ -186,26 +257,18 @@ class HoneyBadgerEpoch:
         e.sync()
         t1 = time.perf_counter()
         times["propose_encode"] = (t1 - t0) * 1e3
-        vall = self._gather(vbuf)                             # [rank][j][p_local] messages
-        vsent_all = self._gather(vsent.view(1, N, m)).view(self.world, N, m)
-        B = int(v_off[-1])
-        g_off = (np.arange(self.world, dtype=np.int64)[:, None] * B + v_off[None, :-1]).reshape(-1)
-        g_off = np.append(g_off, self.world * B)
-        tag, vals, idx, dig, nd, roots, st = e.read_msgs(N, L, vall, g_off)
-        vok = e.validate_table(N, L, vals, idx, dig, nd, roots)
-        j_of = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(m).repeat(self.world)
-        good = ((st == 0) & (tag == _lib.HBG_MSG_VALUE) & (idx == j_of) & (vok == 1)).view(self.world, N, m)
-        good = good & (vsent_all == 1)
-        value_ok = good.permute(0, 2, 1).reshape(N, N)      # [p][j]
+        value_ok, vrecv, run_off, n_val = self._value_round(vbuf, v_off, vsent, per_node)
+        work["value_validations"] = n_val
         e.sync()
         t2 = time.perf_counter()
         times["value"] = (t2 - t1) * 1e3
         # ---- 3. Echo: node j's Echo of p's proof = the Value bytes with variant 1
         runs = []
-        for j in local:
-            lo, hi = m * int(self.msg_len[:j].sum()), m * int(self.msg_len[:j + 1].sum())
-            for r in range(self.world):
-                runs.append(vall[r * B + lo:r * B + hi])
+        for a in range(m):
+            j = r0 + a
+            for rs in range(self.world):
+                lo = run_off(rs, a)
+                runs.append(vrecv[lo:lo + m * int(self.msg_len[j])])
         ebuf = torch.cat(runs).clone()                        # [j local][p] messages of msg_len[j]
         e_len = np.repeat(self.msg_len[r0:r0 + m], N)
         e_off = np.zeros(m * N + 1, np.int64)
@@ -226,29 +289,33 @@ class HoneyBadgerEpoch:
         ge_off = np.zeros(N * N + 1, np.int64)
         ge_off[1:] = np.cumsum(ge_len)
         tag, vals, idx, dig, nd, roots, st = e.read_msgs(N, L, eall, ge_off)
-        eok = e.validate_table(N, L, vals, idx, dig, nd, roots)
         s_of = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(N)
-        echo_ok = ((st == 0) & (tag == _lib.HBG_MSG_ECHO) & (idx == s_of) & (eok == 1)).view(N, N)
-        echo_ok = echo_ok & (esent_all == 1)                  # [s][p]
+        parsed = (st == 0) & (tag == _lib.HBG_MSG_ECHO) & (idx == s_of)
+        # every view validates every echo it receives (hbbft handle_echo)
+        eok = [e.validate_table(N, L, vals, idx, dig, nd, roots) for _ in range(nv)]
+        work["echo_validations"] = nv * N * N
+        echo_ok_v = torch.stack([(parsed & (x == 1)).view(N, N) & (esent_all == 1) for x in eok])   # [v][s][p]
         # echoes per root: the root with the most valid echoes (ties: lowest sender)
         R = roots.view(N, N, 32).permute(1, 0, 2)             # [p][s][32]
-        ok_ps = echo_ok.t()                                   # [p][s]
-        same = (R.unsqueeze(2) == R.unsqueeze(1)).all(-1) & ok_ps.unsqueeze(1)   # [p][s][s']
-        cnt = torch.where(ok_ps, same.sum(-1), torch.full_like(ok_ps, -1, dtype=torch.int64))
-        key = cnt * (N + 1) + (N - torch.arange(N, device=dev))                 # max count, then lowest s
-        best = key.argmax(dim=1)                              # [p]
+        eq = (R.unsqueeze(2) == R.unsqueeze(1)).all(-1)       # [p][s][s']
+        ok_ps = echo_ok_v.permute(0, 2, 1)                    # [v][p][s]
+        cnt_all = torch.einsum("pst,vpt->vps", eq.to(torch.float32), ok_ps.to(torch.float32)).round().to(torch.int64)
+        cnt = torch.where(ok_ps, cnt_all, torch.full_like(cnt_all, -1))
+        key = cnt * (N + 1) + (N - torch.arange(N, device=dev))                  # max count, then lowest s
+        best = key.argmax(dim=2)                              # [v][p]
+        echo_count = cnt.gather(2, best.unsqueeze(2)).squeeze(2).clamp(min=0)   # [v][p]
         ar = torch.arange(N, device=dev)
-        echo_count = cnt[ar, best].clamp(min=0)
-        root_p = R[ar, best]                                  # [p][32]
-        holds = same[ar, best] & ok_ps                        # [p][s] valid echoes carrying root_p
+        root_p = R[ar.unsqueeze(0), best]                     # [v][p][32]
+        holds = eq[ar.unsqueeze(0), best] & ok_ps             # [v][p][s] valid echoes carrying root_p
         e.sync()
         t3 = time.perf_counter()
         times["echo"] = (t3 - t2) * 1e3
-        # ---- 4. Ready
+        # ---- 4. Ready (node j's Readys: its own echo count; every node counts the same messages)
+        rv = (torch.arange(m, device=dev) if per_node else torch.zeros(m, dtype=torch.int64, device=dev))
         rbuf = e.zeros((m, N, 36))
         rbuf[:, :, 0] = _lib.HBG_MSG_READY
-        rbuf[:, :, 4:] = root_p.unsqueeze(0)
-        rsent = (echo_count >= N - f).to(torch.uint8).unsqueeze(0).repeat(m, 1)   # [j local][p]
+        rbuf[:, :, 4:] = root_p[rv]
+        rsent = (echo_count[rv] >= N - f).to(torch.uint8)     # [j local][p]
         for j in faults.silent:
             if j in local:
                 rsent[j - r0] = 0
@@ -256,28 +323,40 @@ class HoneyBadgerEpoch:
         rsent_all = self._gather(rsent)                       # [N j][N p]
         r_off = np.arange(N * N + 1, dtype=np.int64) * 36
         tag, _, _, _, _, rroots, st = e.read_msgs(N, 16, rall, r_off)   # digests only: no value table needed
-        rgood = (st == 0) & (tag == _lib.HBG_MSG_READY)
-        rmatch = (rroots.view(N, N, 32) == root_p.unsqueeze(0)).all(-1) & rgood.view(N, N) & (rsent_all == 1)
-        ready_count = rmatch.sum(0)                           # [p]
-        delivered = (ready_count >= 2 * f + 1) & (echo_count >= N - 2 * f)
-        # ---- 5. decode from the echoes carrying the root
-        D = N - 2 * f
+        rgood = ((st == 0) & (tag == _lib.HBG_MSG_READY)).view(N, N) & (rsent_all == 1)
+        rmatch = (rroots.view(1, N, N, 32) == root_p.unsqueeze(1)).all(-1) & rgood.unsqueeze(0)   # [v][j][p]
+        ready_count = rmatch.sum(1)                           # [v][p]
+        delivered = (ready_count >= 2 * f + 1) & (echo_count >= N - 2 * f)       # [v][p]
+        # ---- 5. decode from the echoes carrying the root: every view its own copy
         S = vals.shape[-1]
         sh = vals.view(N, N, S).permute(1, 0, 2).contiguous()  # [p][s][S]
-        present = (holds & delivered.unsqueeze(1)).to(torch.uint8).contiguous()
-        out, plen, dst = e.decode(N, L, sh, present, root_p.contiguous())
-        out = out[:, :C] if out.shape[1] >= C else torch.nn.functional.pad(out, (0, C - out.shape[1]))
-        le = (out[:, 48:56].to(torch.int64) << (8 * torch.arange(8, device=dev))).sum(1)
-        payload_ok = delivered & (dst == _lib.HBG_DECODE_OK) & (plen == C) & (le == P)
+        present = (holds & delivered.unsqueeze(2)).to(torch.uint8)   # [v][p][s]
+        outs, plens, dsts = [], [], []
+        for c0 in range(0, nv, decode_chunk):
+            c = min(decode_chunk, nv - c0)
+            o, pl, ds = e.decode(N, L, sh.repeat(c, 1, 1), present[c0:c0 + c].reshape(c * N, N).contiguous(),
+                                 root_p[c0:c0 + c].reshape(c * N, 32).contiguous())
+            outs.append(o.view(c, N, -1))
+            plens.append(pl.view(c, N))
+            dsts.append(ds.view(c, N))
+        out, plen, dst = torch.cat(outs), torch.cat(plens), torch.cat(dsts)          # [v][p]...
+        work["decodes"] = nv * N
+        out = out[..., :C] if out.shape[-1] >= C else torch.nn.functional.pad(out, (0, C - out.shape[-1]))
+        le = (out[..., 48:56].to(torch.int64) << (8 * torch.arange(8, device=dev))).sum(-1)
+        payload_ok = delivered & (dst == _lib.HBG_DECODE_OK) & (plen == C) & (le == P)   # [v][p]
+        if not bool((payload_ok == payload_ok[0:1]).all()):
+            # Subset's output is agreed by binary agreement (out of scope): with
+            # full delivery every view must deliver the same set
+            raise RuntimeError("views disagree on the delivered proposals")
         e.sync()
         t4 = time.perf_counter()
         times["ready_decode"] = (t4 - t3) * 1e3
-        # ---- 6/7. Subset accepts; ThresholdDecrypt of every accepted ciphertext
-        acc = torch.nonzero(payload_ok).flatten().tolist()
+        # ---- 6/7. Subset accepts; ThresholdDecrypt of every accepted ciphertext, per view
+        acc = torch.nonzero(payload_ok[0]).flatten().tolist()
         k = len(acc)
         if k:
             at = torch.tensor(acc, device=dev)
-            U, V, W = out[at, :48].contiguous(), out[at, CT_HEAD:CT_HEAD + P].contiguous(), out[at, CT_HEAD + P:C]
+            U, V, W = out[0, at, :48].contiguous(), out[0, at, CT_HEAD:CT_HEAD + P].contiguous(), out[0, at, CT_HEAD + P:C]
             pc = torch.arange(k, dtype=torch.int32, device=dev).repeat_interleave(m)
             pj = torch.arange(m, dtype=torch.int32, device=dev).repeat(k)
             sk_use = self.sk32_local.clone()
@@ -287,23 +366,30 @@ class HoneyBadgerEpoch:
             shares = e.decrypt_shares(U, sk_use, pc, pj).view(k, m, 48)
             sall = self._gather(shares.permute(1, 0, 2).contiguous())   # [N s][k][48]
             share48 = sall.permute(1, 0, 2).contiguous()                # [k][N][48]
-            order = arrival_orders(epoch, acc, N)
             silent = np.array([s in faults.silent for s in range(N)])
-            arr = np.full((k, N), -1, np.int32)
-            for q in range(k):
-                o = order[q][~silent[order[q]]]
-                arr[q, :len(o)] = o
-            V_off = torch.arange(k + 1, dtype=torch.int64, device=dev) * P
-            pt, ct_status, outcome = e.threshold_decrypt(self.t, N, U, V.reshape(-1), V_off, W.contiguous(),
-                                                         self.pk48, share48, torch.from_numpy(arr).to(dev))
-            plaintexts = pt.view(k, P)
+            arr = np.full((nv, k, N), -1, np.int32)
+            for vi, node in enumerate(views):
+                order = arrival_orders(epoch, acc, N, node)
+                for q in range(k):
+                    o = order[q][~silent[order[q]]]
+                    arr[vi, q, :len(o)] = o
+            # view v's instance of ciphertext q: its own copy of (U, V, W) and the N shares
+            V_off = torch.arange(nv * k + 1, dtype=torch.int64, device=dev) * P
+            pt, ct_status, outcome = e.threshold_decrypt(
+                self.t, N, U.repeat(nv, 1), V.repeat(nv, 1).reshape(-1), V_off, W.contiguous().repeat(nv, 1),
+                self.pk48, share48.repeat(nv, 1, 1), torch.from_numpy(arr.reshape(nv * k, N)).to(dev))
+            plaintexts = pt.view(nv, k, P)
+            ct_status = ct_status.view(nv, k)
+            outcome = outcome.view(nv, k, N)
         else:
-            ct_status = torch.zeros(0, dtype=torch.int32, device=dev)
-            plaintexts = e.zeros((0, P))
-            outcome = e.zeros((0, N))
+            ct_status = torch.zeros((nv, 0), dtype=torch.int32, device=dev)
+            plaintexts = e.zeros((nv, 0, P))
+            outcome = e.zeros((nv, 0, N))
+        work["tdec_instances"] = nv * k
+        work["tdec_shares"] = nv * k * N
         e.sync()
         t5 = time.perf_counter()
         times["tdec"] = (t5 - t4) * 1e3
         times["epoch"] = (t5 - t0) * 1e3
-        return EpochResult(value_ok, echo_ok, echo_count, ready_count, delivered, out, payload_ok, acc,
-                           ct_status, plaintexts, outcome, times, self._recv)
+        return EpochResult(value_ok, echo_ok_v[0], echo_count[0], ready_count[0], delivered[0], out[0],
+                           payload_ok[0], acc, views, ct_status, plaintexts, outcome, times, self._recv, work)

@@ -78,6 +78,19 @@ def all_gather_rows(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
     return out
 
 
+def all_to_all_bytes(buf: torch.Tensor, send: list, recv: list, world: int, group=None) -> torch.Tensor:
+    """Personalised exchange of a flat byte buffer: rank-major chunks of
+    send[r] bytes go to rank r, and recv[r] bytes arrive from rank r (one
+    all_to_all_single: RCCL over xGMI with backend "nccl", gloo in the CPU
+    rehearsals).  Without a process group the buffer is returned as is."""
+    if world == 1 and not dist.is_initialized():
+        return buf
+    out = torch.empty(int(sum(recv)), dtype=buf.dtype, device=buf.device)
+    dist.all_to_all_single(out, buf.contiguous(), output_split_sizes=[int(x) for x in recv],
+                           input_split_sizes=[int(x) for x in send], group=group)
+    return out
+
+
 def arrival_mask(instance: int, n: int, epoch: int = 0) -> list:
     """Echo senders whose shard instance `instance` decodes from: the first
     N-f to arrive, in a seeded order (f = (N-1)/3 absent)."""

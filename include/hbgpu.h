@@ -83,15 +83,23 @@ extern "C" {
 
 typedef struct hbg_ctx hbg_ctx;
 
-/* ---- context ---- */
-int hbg_init(hbg_ctx **out, int device); /* device < 0: the current HIP device */
+/* ---- context ----
+ * One context binds ONE device (device < 0: the current HIP device).
+ * Deviation from SURVEY.md §8(b)'s hbg_init(ctx, const int *device_ids, int n):
+ * the engine runs one process per GPU (torch.distributed, RCCL over xGMI),
+ * and instances are sharded across processes, never across the devices of
+ * one context; a multi-device caller opens one context per device. */
+int hbg_init(hbg_ctx **out, int device);
 void hbg_free(hbg_ctx *ctx);
+int hbg_ctx_device(const hbg_ctx *ctx);  /* the device the context binds (< 0: ctx is NULL) */
 /* Enqueue on an external hipStream_t from now on (e.g.
  * torch.cuda.current_stream().cuda_stream); the handle is used verbatim, so
  * NULL selects the HIP null stream.  hbg_reset_stream() returns to the
  * context's own non-blocking stream.  A switch is ordered: work enqueued on
  * the old stream completes before work enqueued on the new one (an event,
- * no host synchronisation). */
+ * no host synchronisation).  An external stream must outlive the switch away
+ * from it; if it was destroyed first, hbg_reset_stream falls back to a
+ * device-wide synchronisation and still returns to the context's stream. */
 int hbg_set_stream(hbg_ctx *ctx, void *hip_stream);
 int hbg_reset_stream(hbg_ctx *ctx);
 int hbg_sync(hbg_ctx *ctx);

@@ -28,6 +28,14 @@ handler.rs:747-764]:
   (tcrypto.threshold_decrypt: set_ciphertext, faults, first t+1 valid,
   late shares ignored).
 
+Two views of the TDec stage (``per_node``): every node runs its own
+ThresholdDecrypt instance of every accepted ciphertext, with its own seeded
+arrival order (the network's per-node work, hbbft's behaviour); or, the
+shared view, one instance per ciphertext on behalf of all nodes.  The RBC
+stages' outcomes are the same at every node under full delivery (every
+node receives the same Values for its index and the same Echoes / Readys),
+so they are restated once.
+
 Faults injected (the same set epoch.py takes): silent nodes (send nothing),
 corrupted Values (p, j), nodes that echo a corrupted value, proposers whose
 ciphertext is corrupted after encryption, nodes that send a share computed
@@ -80,9 +88,15 @@ def encryption_scalar(epoch: int, p: int) -> int:
     return int.from_bytes(b, "little")
 
 
-def arrival_order(epoch: int, p: int, n: int) -> list:
-    """Senders of instance p's decryption shares in arrival order."""
-    rng = synth.SplitMix64(TAG_ARRIVAL, instance_id(epoch, p))
+def arrival_id(epoch: int, p: int, node: int | None = None) -> int:
+    """Seed id of an arrival order: instance p's shared view, or node `node`'s."""
+    return instance_id(epoch, p) | (0 if node is None else (node + 1) << 40)
+
+
+def arrival_order(epoch: int, p: int, n: int, node: int | None = None) -> list:
+    """Senders of instance p's decryption shares in arrival order (at `node`,
+    or the shared view)."""
+    rng = synth.SplitMix64(TAG_ARRIVAL, arrival_id(epoch, p, node))
     keys = [rng.next() for _ in range(n)]
     return sorted(range(n), key=lambda s: (keys[s], s))
 
@@ -107,12 +121,14 @@ class EpochOut:
     delivered: list = field(default_factory=list)    # [p]
     payloads: list = field(default_factory=list)     # [p] decoded bytes or None
     accepted: list = field(default_factory=list)     # proposers of the accepted ciphertexts
-    ct_status: list = field(default_factory=list)    # [k]
-    plaintexts: list = field(default_factory=list)   # [k] bytes or None
-    share_outcome: list = field(default_factory=list)  # [k][s]
+    views: list = field(default_factory=list)        # TDec views: node ids (per node) or [None] (shared)
+    ct_status: list = field(default_factory=list)    # [view][k]
+    plaintexts: list = field(default_factory=list)   # [view][k] bytes or None
+    share_outcome: list = field(default_factory=list)  # [view][k][s]
 
 
-def run_epoch(N: int, P: int, seed: int = 1, epoch: int = 0, faults: Faults = Faults()) -> EpochOut:
+def run_epoch(N: int, P: int, seed: int = 1, epoch: int = 0, faults: Faults = Faults(),
+              per_node: bool = True) -> EpochOut:
     f = rbc.num_faulty(N)
     t = f
     coeffs, sks = keyset(N, t, seed)
@@ -176,6 +192,7 @@ def run_epoch(N: int, P: int, seed: int = 1, epoch: int = 0, faults: Faults = Fa
             payload = rbc.decode_from_shards(leaves, N, root)
         out.payloads.append(payload)
     # ---- Subset accepts the delivered instances; ThresholdDecrypt each ciphertext
+    cts = []
     for p in range(N):
         if not out.delivered[p] or out.payloads[p] is None:
             continue
@@ -184,17 +201,30 @@ def run_epoch(N: int, P: int, seed: int = 1, epoch: int = 0, faults: Faults = Fa
             continue
         out.accepted.append(p)
         try:
-            ct = T.Ciphertext(B.g1_decompress(parts[0]), parts[1], B.g2_decompress(parts[2]))
+            cts.append(T.Ciphertext(B.g1_decompress(parts[0]), parts[1], B.g2_decompress(parts[2])))
         except ValueError:
-            out.ct_status.append(T.E_INVALID_CIPHERTEXT)
-            out.plaintexts.append(None)
-            out.share_outcome.append([T.SHARE_NONE] * N)
-            continue
-        shares = [None if s in faults.silent else
-                  T.decrypt_share(sks[(s + 1) % N] if s in faults.bad_share else sks[s], ct) for s in range(N)]
-        order = [s for s in arrival_order(epoch, p, N) if s not in faults.silent]
-        st, pt, oc = T.threshold_decrypt(t, ct, pk_shares, shares, order)
-        out.ct_status.append(st)
-        out.plaintexts.append(pt)
-        out.share_outcome.append(list(oc))
+            cts.append(None)
+    shares = []   # [k][s]: every node's decryption share of each accepted ciphertext
+    for ct in cts:
+        shares.append(None if ct is None else
+                      [None if s in faults.silent else
+                       T.decrypt_share(sks[(s + 1) % N] if s in faults.bad_share else sks[s], ct) for s in range(N)])
+    caches = [{} for _ in cts]   # verdicts are the same at every node: computed once per ciphertext
+    out.views = list(range(N)) if per_node else [None]
+    for node in out.views:
+        st_v, pt_v, oc_v = [], [], []
+        for q, (p, ct) in enumerate(zip(out.accepted, cts)):
+            if ct is None:
+                st_v.append(T.E_INVALID_CIPHERTEXT)
+                pt_v.append(None)
+                oc_v.append([T.SHARE_NONE] * N)
+                continue
+            order = [s for s in arrival_order(epoch, p, N, node) if s not in faults.silent]
+            st, pt, oc = T.threshold_decrypt(t, ct, pk_shares, shares[q], order, cache=caches[q])
+            st_v.append(st)
+            pt_v.append(pt)
+            oc_v.append(list(oc))
+        out.ct_status.append(st_v)
+        out.plaintexts.append(pt_v)
+        out.share_outcome.append(oc_v)
     return out

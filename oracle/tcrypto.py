@@ -227,7 +227,7 @@ ARRIVAL_CIPHERTEXT = 0xFFFFFFFE  # arrival entry: set_ciphertext + start_decrypt
 E_NOT_ENOUGH_SHARES, E_INVALID_CIPHERTEXT = -20, -23
 
 
-def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arrival=None):
+def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arrival=None, cache=None):
     """One node's hbbft ThresholdDecrypt instance [EXT, hbbft
     src/threshold_decrypt.rs, recalled from upstream: parity unpinned],
     restated.
@@ -253,7 +253,12 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
         unchecked (SHARE_IGNORED); fewer than t+1 valid shares:
         E_NOT_ENOUGH_SHARES.
     shares[i]: sender i's share (G1 point or None).  Returns (status,
-    plaintext or None, outcome per sender)."""
+    plaintext or None, outcome per sender).  cache: a dict shared by the
+    instances of ONE ciphertext with the same shares (every node's own
+    ThresholdDecrypt of it, oracle/epoch.py): verdicts and combinations are
+    computed once (a memo of pure functions, not a change of semantics)."""
+    if cache is None:
+        cache = {}
     n = len(pk_shares)
     order = list(range(n)) if arrival is None else list(arrival)
     for j, s in enumerate(order):
@@ -261,11 +266,15 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
             order = order[:j]
             break
     outcome = [SHARE_NONE] * n
-    ct_ok = ct.verify()
-    h = hash_g1_g2(ct.U, ct.V) if ct_ok else None
+    if "ct_ok" not in cache:
+        cache["ct_ok"] = ct.verify()
+        cache["h"] = hash_g1_g2(ct.U, ct.V) if cache["ct_ok"] else None
+    ct_ok, h = cache["ct_ok"], cache["h"]
 
     def valid(s):
-        return shares[s] is not None and verify_decryption_share(pk_shares[s], shares[s], ct, h)
+        if ("v", s) not in cache:
+            cache[("v", s)] = shares[s] is not None and verify_decryption_share(pk_shares[s], shares[s], ct, h)
+        return cache[("v", s)]
 
     ct_set = ARRIVAL_CIPHERTEXT not in order
     if ct_set and not ct_ok:
@@ -308,5 +317,7 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
         term = len(held) == t + 1
     if not term:
         return E_NOT_ENOUGH_SHARES, None, outcome
-    sel = sorted(held)[: t + 1]
-    return 0, decrypt(t, [(i, shares[i]) for i in sel], ct), outcome
+    sel = tuple(sorted(held)[: t + 1])
+    if ("d", sel) not in cache:
+        cache[("d", sel)] = decrypt(t, [(i, shares[i]) for i in sel], ct)
+    return 0, cache[("d", sel)], outcome

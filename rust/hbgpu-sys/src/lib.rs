@@ -61,6 +61,7 @@ pub const HBG_WIRE_MAX_FRAME: u32 = 8 * 1024 * 1024;
 extern "C" {
     pub fn hbg_init(out: *mut *mut hbg_ctx, device: c_int) -> c_int;
     pub fn hbg_free(ctx: *mut hbg_ctx);
+    pub fn hbg_ctx_device(ctx: *const hbg_ctx) -> c_int;
     pub fn hbg_set_stream(ctx: *mut hbg_ctx, hip_stream: *mut c_void) -> c_int;
     pub fn hbg_reset_stream(ctx: *mut hbg_ctx) -> c_int;
     pub fn hbg_sync(ctx: *mut hbg_ctx) -> c_int;

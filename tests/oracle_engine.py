@@ -132,6 +132,7 @@ class OracleEngine:
     def threshold_decrypt(self, t, N, U, V, V_off, W, pk48, share48, arrival):
         k = U.shape[0]
         pks = [B.g1_decompress(_b(p)) for p in pk48]
+        memo = {}   # one verdict memo per distinct (ciphertext, shares): the per-node views repeat them
         pt = np.zeros(max(int(V.numel()), 1), np.uint8)
         st = np.zeros(k, np.int32)
         oc = np.zeros((k, N), np.uint8)
@@ -149,7 +150,8 @@ class OracleEngine:
                     shares.append(B.g1_decompress(_b(share48[q, s])))
                 except ValueError:
                     shares.append(None)
-            s_, p_, o_ = T.threshold_decrypt(t, ct, pks, shares, order)
+            key = (_b(U[q]), v, _b(W[q]), _b(share48[q]))
+            s_, p_, o_ = T.threshold_decrypt(t, ct, pks, shares, order, cache=memo.setdefault(key, {}))
             st[q] = s_
             oc[q] = o_
             if s_ == 0:

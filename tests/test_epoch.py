@@ -52,12 +52,17 @@ def compare(res: hbe.EpochResult, exp: oep.EpochOut, P: int):
         if exp.payloads[p] is not None:
             assert pays[p, :C].tobytes() == exp.payloads[p], p
     assert res.accepted == exp.accepted
-    assert _np(res.ct_status).tolist() == exp.ct_status
-    pts = _np(res.plaintexts)
-    for q, pt in enumerate(exp.plaintexts):
-        if pt is not None:
-            assert pts[q].tobytes() == pt, q
-    assert _np(res.share_outcome).tolist() == exp.share_outcome
+    # TDec views: this rank's nodes (each its own ThresholdDecrypt with its own
+    # arrival order) or the shared view
+    assert len(res.views) == _np(res.ct_status).shape[0]
+    for vi, node in enumerate(res.views):
+        ei = exp.views.index(None if node < 0 else node)
+        assert _np(res.ct_status)[vi].tolist() == exp.ct_status[ei], node
+        pts = _np(res.plaintexts)[vi]
+        for q, pt in enumerate(exp.plaintexts[ei]):
+            if pt is not None:
+                assert pts[q].tobytes() == pt, (node, q)
+        assert _np(res.share_outcome)[vi].tolist() == exp.share_outcome[ei], node
 
 
 # ----------------------------------------------------------------------------- oracle sanity
@@ -65,12 +70,21 @@ def test_oracle_epoch_honest_delivers_every_contribution():
     N, P = 4, 40
     out = oep.run_epoch(N, P, seed=3)
     assert out.delivered == [True] * N and out.accepted == list(range(N))
-    assert out.ct_status == [0] * N
-    for p in range(N):
-        assert out.plaintexts[p] == synth.synth_bytes(oep.TAG_CONTRIB, oep.instance_id(0, p), P)
-    f = (N - 1) // 3
-    for oc in out.share_outcome:  # exactly t+1 = f+1 accepted, the rest ignored
-        assert oc.count(1) == f + 1 and oc.count(3) == N - f - 1
+    assert out.views == list(range(N))
+    for v in range(N):  # every node decrypts every contribution
+        assert out.ct_status[v] == [0] * N
+        for p in range(N):
+            assert out.plaintexts[v][p] == synth.synth_bytes(oep.TAG_CONTRIB, oep.instance_id(0, p), P)
+        f = (N - 1) // 3
+        for oc in out.share_outcome[v]:  # exactly t+1 = f+1 accepted, the rest ignored
+            assert oc.count(1) == f + 1 and oc.count(3) == N - f - 1
+    # each node handles shares in its own arrival order: the views differ
+    assert len({str(out.share_outcome[v]) for v in range(N)}) > 1
+
+
+def test_oracle_epoch_shared_view_is_one_instance_per_ciphertext():
+    out = oep.run_epoch(4, 40, seed=3, per_node=False)
+    assert out.views == [None] and len(out.ct_status) == 1 and out.ct_status[0] == [0] * 4
 
 
 def test_oracle_epoch_fault_semantics():
@@ -81,22 +95,28 @@ def test_oracle_epoch_fault_semantics():
     assert not any(out.echo_ok[3])                   # the silent node echoes nothing
     assert not out.delivered[3]                      # ... and proposes nothing
     k6 = out.accepted.index(6)
-    assert out.ct_status[k6] == oep.T.E_INVALID_CIPHERTEXT
-    for q, p in enumerate(out.accepted):
-        if p != 6:
-            assert out.ct_status[q] == 0
-            assert out.share_outcome[q][3] == 0      # silent: no share
-            assert out.share_outcome[q][5] in (0, 2, 3)  # bad share: fault if processed, never accepted
+    for v in out.views:
+        assert out.ct_status[v][k6] == oep.T.E_INVALID_CIPHERTEXT
+        for q, p in enumerate(out.accepted):
+            if p != 6:
+                assert out.ct_status[v][q] == 0
+                assert out.share_outcome[v][q][3] == 0      # silent: no share
+                assert out.share_outcome[v][q][5] in (0, 2, 3)  # bad share: fault if processed, never accepted
 
 
 # ----------------------------------------------------------------------------- product orchestration on CPU
+@pytest.mark.parametrize("per_node", [True, False])
 @pytest.mark.parametrize("name,N,P", [("honest", 4, 40), ("faulty", 7, 24)])
-def test_epoch_world1_oracle_engine(name, N, P):
+def test_epoch_world1_oracle_engine(name, N, P, per_node):
     from tests.oracle_engine import OracleEngine
     ep = hbe.HoneyBadgerEpoch(N, P, OracleEngine(), seed=2)
-    res = ep.run(epoch=1, faults=_faults(FAULTS[name], hbe))
-    compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep)), P)
+    res = ep.run(epoch=1, faults=_faults(FAULTS[name], hbe), per_node=per_node)
+    compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep), per_node=per_node), P)
     assert res.exchange_bytes == 0
+    nv = N if per_node else 1
+    assert res.views == (list(range(N)) if per_node else [-1])
+    assert res.work["echo_validations"] == nv * N * N and res.work["decodes"] == nv * N
+    assert res.work["value_validations"] == N * N
 
 
 def test_epoch_gloo_world1_group_runs_the_collective():
@@ -153,22 +173,32 @@ def test_epoch_gloo_world2(name, N, P):
         p.join(timeout=60)
         assert p.exitcode == 0
     exp = oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep))
+    m = N // 2
     for r in range(2):
         compare(got[r], exp, P)
         assert got[r].exchange_bytes > 0
+        assert got[r].views == list(range(r * m, (r + 1) * m))
+        # each rank validates only the Values addressed to its own nodes (N per
+        # node), every echo once per local node, and decodes / decrypts per node
+        assert got[r].work["value_validations"] == N * m
+        assert got[r].work["echo_validations"] == m * N * N
+        assert got[r].work["decodes"] == m * N
+        assert got[r].work["tdec_instances"] == m * len(exp.accepted)
 
 
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,N,P", [("honest", 4, 40), ("faulty", 7, 24), ("faulty", 16, 300)])
-def test_epoch_device_world1(name, N, P):
+@pytest.mark.parametrize("name,N,P,per_node", [("honest", 4, 40, True), ("faulty", 7, 24, True),
+                                               ("faulty", 16, 300, True), ("faulty", 16, 300, False)])
+def test_epoch_device_world1(name, N, P, per_node):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from hydrabadger_amd import network
     eng = network.DeviceEngine(torch.device("cuda:0"))
     try:
-        res = hbe.HoneyBadgerEpoch(N, P, eng, seed=2).run(epoch=1, faults=_faults(FAULTS[name], hbe))
-        compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep)), P)
+        res = hbe.HoneyBadgerEpoch(N, P, eng, seed=2).run(epoch=1, faults=_faults(FAULTS[name], hbe),
+                                                           per_node=per_node)
+        compare(res, oep.run_epoch(N, P, seed=2, epoch=1, faults=_faults(FAULTS[name], oep), per_node=per_node), P)
     finally:
         eng.ctx.close()
 
@@ -206,12 +236,13 @@ def test_epoch_device_n64_honest_plaintexts():
         N, P = 64, 4096
         res = hbe.HoneyBadgerEpoch(N, P, eng, seed=5).run(epoch=2)
         assert bool(res.delivered.all()) and res.accepted == list(range(N))
-        assert _np(res.ct_status).tolist() == [0] * N
+        assert res.views == list(range(N)) and (_np(res.ct_status) == 0).all()
         pts = _np(res.plaintexts)
-        for p in (0, 31, 63):
-            assert pts[p].tobytes() == synth.synth_bytes(hbe.TAG_CONTRIB, hbe.instance_id(2, p), P)
+        for v in (0, 17, 63):
+            for p in (0, 31, 63):
+                assert pts[v, p].tobytes() == synth.synth_bytes(hbe.TAG_CONTRIB, hbe.instance_id(2, p), P)
         oc = _np(res.share_outcome)
-        assert ((oc == 1).sum(1) == 22).all() and ((oc == 3).sum(1) == N - 22).all()
+        assert ((oc == 1).sum(2) == 22).all() and ((oc == 3).sum(2) == N - 22).all()
     finally:
         eng.ctx.close()
 
@@ -241,10 +272,10 @@ def test_epoch_device_configs4_size():
         N, P = 128, 1 << 20
         res = hbe.HoneyBadgerEpoch(N, P, eng, seed=7).run(epoch=3)
         assert bool(res.delivered.all()) and res.accepted == list(range(N))
-        assert _np(res.ct_status).tolist() == [0] * N
+        assert res.views == list(range(N)) and (_np(res.ct_status) == 0).all()
         want = eng.synth(hbe.TAG_CONTRIB, hbe.instance_id(3, 0), N, P)
-        assert torch.equal(res.plaintexts, want)
+        assert len(res.views) == N and all(torch.equal(res.plaintexts[v], want) for v in range(N))
         oc = _np(res.share_outcome)
-        assert ((oc == 1).sum(1) == 43).all() and ((oc == 3).sum(1) == N - 43).all()
+        assert ((oc == 1).sum(2) == 43).all() and ((oc == 3).sum(2) == N - 43).all()
     finally:
         eng.ctx.close()

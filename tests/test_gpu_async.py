@@ -295,3 +295,36 @@ def test_device_mode_proof_msgs_index_check():
         o = out.cpu().numpy()
         assert (o[int(off[2]):int(off[4])] == 0xEE).all()            # both bad messages unwritten
         assert o[int(off[0]):int(off[0]) + 4].tobytes() == struct.pack("<I", 0)
+
+
+@pytest.mark.gpu
+def test_oversized_tdec_batches_refused_before_anything_runs():
+    """A batch larger than one grid (2^32 work-items) is HBG_E_ARG before any
+    staging or launch: the outputs stay untouched and the context
+    still works afterwards."""
+    torch = _torch()
+    from hydrabadger_amd import _lib
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(dev)
+    ctx = _ctx_on(torch, stream)
+    with torch.cuda.stream(stream):
+        pk = torch.zeros(48, dtype=torch.uint8, device=dev)
+        r32 = torch.zeros(32, dtype=torch.uint8, device=dev)
+        off = torch.zeros(2, dtype=torch.int64, device=dev)
+        U = torch.full((48,), 0xAB, dtype=torch.uint8, device=dev)
+        W = torch.full((96,), 0xCD, dtype=torch.uint8, device=dev)
+        n = 1 << 32                                   # (n + 63) / 64 blocks x 64 > 2^32 - 1 work-items
+        rc = _lib.lib().hbg_tdec_encrypt(ctx.h, pk.data_ptr(), n, r32.data_ptr(), r32.data_ptr(), off.data_ptr(),
+                                         U.data_ptr(), U.data_ptr(), W.data_ptr(), _lib.HBG_DEVICE)
+        assert rc == _lib.HBG_E_ARG
+        sh = torch.zeros(48, dtype=torch.uint8, device=dev)
+        ix = torch.zeros(1, dtype=torch.int32, device=dev)
+        out = torch.full((16,), 0xEF, dtype=torch.uint8, device=dev)
+        st = torch.full((1,), 7, dtype=torch.int32, device=dev)
+        rc = _lib.lib().hbg_tdec_combine(ctx.h, 1, (1 << 26) + 1, sh.data_ptr(), ix.data_ptr(), out.data_ptr(),
+                                         off.data_ptr(), out.data_ptr(), st.data_ptr(), _lib.HBG_DEVICE)
+        assert rc == _lib.HBG_E_ARG
+        torch.cuda.synchronize(dev)
+        assert (U.cpu() == 0xAB).all() and (W.cpu() == 0xCD).all()
+        assert (out.cpu() == 0xEF).all() and st.cpu().tolist() == [7]
+        assert _lib.lib().hbg_sync(ctx.h) == 0

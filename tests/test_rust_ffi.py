@@ -18,6 +18,7 @@ LIB_RS = os.path.join(ROOT, "rust", "hbgpu-sys", "src", "lib.rs")
 C_TO_RUST = {
     "int": "c_int", "uint32_t": "u32", "uint64_t": "u64", "int32_t": "i32", "void": None,
     "hbg_ctx*": "*mut hbg_ctx", "hbg_ctx**": "*mut *mut hbg_ctx", "void*": "*mut c_void",
+    "const hbg_ctx*": "*const hbg_ctx",
     "const char*": "*const c_char", "char*": "*mut c_char",
     "const uint8_t*": "*const u8", "uint8_t*": "*mut u8",
     "const uint32_t*": "*const u32", "uint32_t*": "*mut u32",

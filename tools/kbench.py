@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--payload", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--splits", default="0,1",
+                    help="decode schedules to time (hbg_test_set_rs_split): 0 one-pass, 1 data rows + constant "
+                         "parity encoder, -1 the library default")
     a = ap.parse_args()
     from hydrabadger_amd import _lib, workload
     from hydrabadger_amd import broadcast as bc
@@ -89,7 +92,7 @@ def main():
             out = torch.empty((B, OS), dtype=torch.uint8, device=dev)
             dpl = torch.empty(B, dtype=torch.int64, device=dev)
             dst = torch.empty(B, dtype=torch.uint8, device=dev)
-            for split in (0, 1):  # hbg_test_set_rs_split: one-pass coder / data rows + constant parity encoder
+            for split in [int(x) for x in a.splits.split(",")]:  # hbg_test_set_rs_split
                 _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, split))
                 res[f"decode_split{split}_ms"] = t(lambda: bc.rbc_decode_batch(
                     N, L, shards, present, roots, out, dpl, dst, ctx=ctx, device=True, asynchronous=True))
