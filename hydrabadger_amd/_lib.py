@@ -96,6 +96,7 @@ SIGNATURES = {
     "hbg_test_set_tdec_batched": (_i, [_vp, C.c_int]),
     "hbg_test_set_rbc_fused": (_i, [_vp, C.c_int]),
     "hbg_test_set_rs_split": (_i, [_vp, C.c_int]),
+    "hbg_test_set_rbc_decode_fused": (_i, [_vp, C.c_int]),
     "hbg_test_set_latency_lanes": (C.c_uint64, [C.c_uint64]),
 }
 

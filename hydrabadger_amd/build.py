@@ -12,6 +12,7 @@ import argparse
 import concurrent.futures as cf
 import glob
 import os
+import re
 import subprocess
 import sys
 
@@ -25,11 +26,19 @@ CFLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fconstexpr-s
           "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 
 
+def _local_includes(path: str, seen: set) -> set:
+    """Every quoted #include reachable from `path` (a translation unit may
+    include another .hip: tdec_kernels_lat.hip)."""
+    for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', open(path).read(), flags=re.M):
+        dep = os.path.normpath(os.path.join(os.path.dirname(path), m.group(1)))
+        if os.path.exists(dep) and dep not in seen:
+            seen.add(dep)
+            _local_includes(dep, seen)
+    return seen
+
+
 def _deps_mtime(src: str) -> float:
-    # a translation unit may include another .hip (tdec_kernels_lat.hip)
-    hdrs = (glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.hip")) +
-            glob.glob(os.path.join(PKG, "..", "include", "*.h")))
-    return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in hdrs])
+    return max(os.path.getmtime(f) for f in _local_includes(src, {src}))
 
 
 def _compile(src: str, force: bool) -> str:

@@ -55,6 +55,9 @@ struct hbg_ctx {
     // run-time coder then missing parity rows by the constant encoder where one
     // exists; 0 every missing row by the run-time coder; -1 (default) 1 for Q > 16
     int rs_split = -1;
+    // hbg_rbc_decode schedule (hbg_test_set_rbc_decode_fused): 0 plan -> coder(s) -> merkle_build, 1 / -1
+    // (default) the fused rbc_decode_merkle where it exists ((D, Q) = (22, 42), N = 64)
+    int dec_fused = -1;
     int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
     hipEvent_t switch_ev = nullptr;  // hbg_set_stream: orders the new stream after the old one
     // a second stream for independent launches inside one call (fork / join by events)
@@ -250,6 +253,23 @@ int reconstruct_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* 
     if (status_dev)
         HBG_TRY(hipMemcpy2DAsync(status_dev, sizeof(int32_t), plans, ps, sizeof(int32_t), n, hipMemcpyDeviceToDevice,
                                  c->stream));
+    return HBG_OK;
+}
+
+// hbg_rbc_decode's reconstruct + Merkle rebuild in one kernel (rbc_decode_merkle,
+// after rs_plan's data-only plan); the plan status goes to status_dev.
+int decode_fused_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t S,
+                        const uint8_t* present_dev, uint64_t n, int32_t* status_dev, uint8_t* levels) {
+    uint8_t* mat = nullptr;
+    HBG_CHECK(device_matrix(c, D, Q, &mat));
+    const uint64_t ps = plan_stride(D, Q);
+    void* plans = nullptr;
+    HBG_CHECK(scratch(c, 11, ps * n, &plans));
+    HBG_TRY(launch_rs_plan(present_dev, D, Q, D, n, mat, (uint8_t*)plans, ps, c->stream));
+    HBG_TRY(launch_rbc_decode_merkle(D, Q, shards, S, L, n, present_dev, (const uint8_t*)plans, ps, levels,
+                                     c->stream));
+    HBG_TRY(hipMemcpy2DAsync(status_dev, sizeof(int32_t), plans, ps, sizeof(int32_t), n, hipMemcpyDeviceToDevice,
+                             c->stream));
     return HBG_OK;
 }
 
@@ -593,13 +613,18 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
         void *dl = nullptr, *ds = nullptr;
         HBG_CHECK(scratch(c, 9, (size_t)nodes * 32 * n, &dl));
         HBG_CHECK(scratch(c, 10, sizeof(int32_t) * n, &ds));
-        if (Q) {
-            HBG_CHECK(reconstruct_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds));
+        const bool fused = Q && c->dec_fused != 0 && has_fused_decoder(D, Q) && const_encoder_fits(D, Q, S, 0, false);
+        if (fused) {
+            HBG_CHECK(decode_fused_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds, (uint8_t*)dl));
         } else {
-            // Trivial coding: every shard must be present (hbbft Coding::reconstruct_shards)
-            HBG_TRY(launch_rbc_trivial_status(n, N, dpres, (int32_t*)ds, c->stream));
+            if (Q) {
+                HBG_CHECK(reconstruct_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds));
+            } else {
+                // Trivial coding: every shard must be present (hbbft Coding::reconstruct_shards)
+                HBG_TRY(launch_rbc_trivial_status(n, N, dpres, (int32_t*)ds, c->stream));
+            }
+            HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream));
         }
-        HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream));
         HBG_TRY(launch_rbc_glue(dsh, S, L, N, D, n, (const uint8_t*)dl, droots, (const int32_t*)ds, dplen, dstat, dout,
                                 dos, c->stream));
         return HBG_OK;
@@ -1329,6 +1354,13 @@ int hbg_test_set_rs_split(hbg_ctx* c, int on) {
     if (!c || on < -1 || on > 1) return HBG_E_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     c->rs_split = on;
+    return HBG_OK;
+}
+
+int hbg_test_set_rbc_decode_fused(hbg_ctx* c, int on) {
+    if (!c || on < -1 || on > 1) return HBG_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->dec_fused = on;
     return HBG_OK;
 }
 

@@ -92,6 +92,12 @@ hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint32
 hipError_t launch_rs_encode_missing(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                     const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
                                     hipStream_t st);
+// Fused reconstruct + Merkle rebuild after a data-only plan (rs_plan max_row =
+// D): missing data rows, missing parity rows and the levels in one launch.
+bool has_fused_decoder(uint32_t D, uint32_t Q);
+hipError_t launch_rbc_decode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                    const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
+                                    uint8_t* levels, hipStream_t st);
 hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
                                uint8_t* levels, hipStream_t st);
 hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,

@@ -824,6 +824,276 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     }
 }
 
+// ============================================================== fused decode_from_shards
+// rbc_decode_merkle<D,Q>: hbbft decode_from_shards' reconstruct (a7: rse
+// reconstruct_shards — missing data rows from the first D present rows with
+// the per-instance inverse, then the missing parity rows re-encoded from the
+// completed data rows; present rows kept as received) and the Merkle rebuild
+// over all N rows (MerkleTree::from_vec) in ONE launch — the decode twin of
+// rbc_encode_merkle.  One wave per instance (LPI = 64 = N):
+//   coding pass  lane = column: the D input words (first D present rows,
+//                rs_plan's data-only plan), the missing data words by the
+//                run-time split-nibble coder (wave-uniform coefficients,
+//                v_movrels selects, as rs_code_movrel), the data words of the
+//                instance (present: an input word, missing: a rebuilt one —
+//                uniform register selects), the Q parity words by the
+//                compile-time encoder; every MISSING row's word is stored to
+//                its shard row and to its slot of the LDS ring (slot = rank of
+//                the row among the missing rows: <= Q slots when decodable);
+//   absorb       lane = row: every completed 136-byte block — a missing row
+//                from the ring, a present row straight from its shard row
+//                (not written by this kernel);
+// then the leaf digests and the tree in LDS, levels written like
+// merkle_build's.  Root check and glue stay in rbc_glue_status / _copy.
+// An instance whose plan failed (fewer than D rows present) is left alone
+// (no rows, no levels): the glue reports None from the plan status.
+// Replaces rs_code_movrel -> rs_encode_missing -> merkle_build, whose
+// Merkle pass re-read all N rows (25 GB per 8,192 x 1 MiB).
+template <int D, int Q>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint64_t n,
+                       const uint8_t* __restrict__ present, const uint8_t* __restrict__ plans, uint64_t plan_stride,
+                       uint8_t* __restrict__ levels) {
+    static_assert(D + Q == 64, "one wave per instance, lane = row");
+    constexpr uint32_t N = D + Q, NODES = merkle_nodes(N);
+    constexpr uint32_t R = fused_ring_bytes(4 * 64);
+    typedef const __attribute__((address_space(4))) uint32_t* cu32;  // scalar (SMEM) loads
+    typedef uint32_t v32 __attribute__((ext_vector_type(32)));      // dynamic uniform index -> v_movrels
+    __shared__ __attribute__((aligned(16))) uint64_t lds[(Q * R > NODES * 32 ? Q * R : NODES * 32) / 8];
+    uint32_t* ring = reinterpret_cast<uint32_t*>(lds);
+    uint32_t* tree = reinterpret_cast<uint32_t*>(lds);
+    const uint32_t t = threadIdx.x;
+    const uint64_t inst = blockIdx.x;
+    if (inst >= n) return;
+    const uint8_t* pbase = plans + inst * plan_stride;
+    const CodePlan* plan = reinterpret_cast<const CodePlan*>(pbase);
+    if (__builtin_amdgcn_readfirstlane(plan->status) != 0) return;  // too few present: decode is None
+    const uint32_t n_out = __builtin_amdgcn_readfirstlane(plan->n_out);
+    const uint64_t miss = __ballot(present[inst * N + t] == 0);      // bit r: row r is missing
+    const uint64_t miss_data = miss & ((1ull << D) - 1ull);
+    const uint64_t pres_data = ~miss & ((1ull << D) - 1ull);
+    uint8_t* base = shards + inst * (uint64_t)N * S;
+    const __amdgpu_buffer_rsrc_t rows = raw_rsrc(base);
+    const uint32_t qp = plan_qpad(Q);
+    const cu32 offs = (cu32)(pbase + plan_offs_at(D, Q));
+    uint32_t in_off[D];  // byte offset of input row j (wave-uniform)
+#pragma unroll
+    for (int j = 0; j < D; ++j) in_off[j] = __builtin_amdgcn_readfirstlane((uint32_t)plan->in_idx[j]) * (uint32_t)S;
+    const uint64_t cols = (L + 3) / 4;
+    const uint32_t passes = (uint32_t)((cols + 63) / 64);
+    auto slot_of = [&](uint32_t row) { return (uint32_t)__builtin_popcountll(miss & ((1ull << row) - 1ull)); };
+    const bool row_missing = (miss >> t) & 1ull;
+    const uint64_t* rrow = reinterpret_cast<const uint64_t*>(ring + (row_missing ? slot_of(t) : 0u) * (R / 4));
+    u64p a[25];
+    keccak_zero(a);
+    uint32_t done = 0;
+    // words [0, nw) of the 136-byte block of row t at byte 136 * done (a
+    // shard row is read only below round_up(L, 8) <= S)
+    auto load_block = [&](uint64_t (&w)[17], uint32_t nw) {
+        if (row_missing) {
+            const uint32_t rp = (136u * done) % R / 8;
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w[i] = rrow[rp + i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                w[i] = 0;
+                if ((uint32_t)i < nw) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rows, t * (uint32_t)S + 8 * i, 136 * done, 0);
+                    w[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+                }
+            }
+        }
+    };
+    uint32_t pre[D];  // the next pass's input words, loaded during this pass's Keccak work
+    bool have_pre = false;
+    auto load_inputs = [&](uint32_t p0, uint32_t (&w)[D]) {
+        const uint32_t vo = 4 * t;
+#pragma unroll
+        for (int j = 0; j < D; ++j) w[j] = __builtin_amdgcn_raw_buffer_load_b32(rows, vo, in_off[j] + 4 * p0, 0);
+    };
+    for (uint32_t ps = 0; ps < passes; ++ps) {
+        const uint32_t p0 = ps * 64, p = p0 + t;
+        const bool active = 4 * (uint64_t)p < L;
+        uint32_t wpos = (uint32_t)(((uint64_t)ps * 256) % R) + 4 * t;
+        if (wpos >= R) wpos -= R;
+        uint32_t* rcol = ring + wpos / 4;
+        if (active) {
+            uint32_t win[D];
+            if (have_pre) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) win[j] = pre[j];
+            } else {
+                load_inputs(p0, win);
+            }
+            // ---- missing data rows: run-time coefficients over the D inputs
+            v32 acc;
+#pragma unroll
+            for (int o = 0; o < 32; ++o) acc[o] = 0u;
+            v32 wv;
+#pragma unroll
+            for (int j = 0; j < D; ++j) wv[j] = win[j];
+#pragma unroll
+            for (int j = D; j < 32; ++j) wv[j] = 0u;
+            if (n_out) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    uint32_t wj = win[j];
+                    asm volatile("" : "+v"(wj));
+                    const NibPair T = nib_tables(wj);
+                    typedef uint32_t v16 __attribute__((ext_vector_type(16)));
+                    v16 tl, th;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        tl[e] = T.lo.t[e];
+                        th[e] = T.hi.t[e];
+                    }
+                    const cu32 oj = offs + 2 * (uint64_t)j * qp;
+                    // rows in groups of 4, a group only while o0 < n_out (wave-uniform);
+                    // rows o >= n_out inside a group point at the zero entries (rs_plan's padding)
+#pragma unroll
+                    for (int o0 = 0; o0 < D; o0 += 4) {
+                        if ((uint32_t)o0 < n_out) {
+#pragma unroll
+                            for (int o = o0; o < (o0 + 4 < D ? o0 + 4 : D); ++o) {
+                                const uint32_t lo = oj[2 * o] >> 8, hi = (oj[2 * o + 1] >> 8) - 16u;
+                                acc[o] = xor3u(acc[o], tl[lo & 15u], th[hi & 15u]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int o = 0; o < D; ++o) asm volatile("" : "+v"(acc[o]));
+                }
+            }
+            // ---- the instance's data words: present -> its input word, missing -> rebuilt
+            uint32_t d[D];
+#pragma unroll
+            for (int J = 0; J < D; ++J) {
+                const uint32_t below = (uint32_t)((1ull << J) - 1ull);
+                if ((miss_data >> J) & 1ull) {
+                    const uint32_t o = (uint32_t)__builtin_popcountll(miss_data & below);
+                    d[J] = acc[o];
+                    __builtin_amdgcn_raw_buffer_store_b32(d[J], rows, 4 * t, J * (uint32_t)S + 4 * p0, 0);
+                    rcol[slot_of(J) * (R / 4)] = d[J];
+                } else {
+                    d[J] = wv[(uint32_t)__builtin_popcountll(pres_data & below)];
+                }
+            }
+            // ---- parity: the compile-time encoder over the data words; missing rows stored
+            uint32_t accp[Q];
+#pragma unroll
+            for (int k = 0; k < Q; ++k) accp[k] = 0u;
+            [&]<int... J>(std::integer_sequence<int, J...>) {
+                (([&] {
+                    uint32_t w = d[J];
+                    asm volatile("" : "+v"(w));
+                    const NibPair T = nib_tables(w);
+                    mac_column<D, Q, J>(accp, T, std::make_integer_sequence<int, Q>{});
+#pragma unroll
+                    for (int k = 0; k < Q; ++k) asm volatile("" : "+v"(accp[k]));
+                }()), ...);
+            }(std::make_integer_sequence<int, D>{});
+#pragma unroll
+            for (int k = 0; k < Q; ++k) {
+                if ((miss >> (D + k)) & 1ull) {
+                    __builtin_amdgcn_raw_buffer_store_b32(accp[k], rows, 4 * t, (D + k) * (uint32_t)S + 4 * p0, 0);
+                    rcol[slot_of(D + k) * (R / 4)] = accp[k];
+                }
+            }
+        }
+        __syncthreads();  // the pass's ring words are visible to every row lane
+        const uint64_t written = 256ull * (ps + 1);
+        const uint64_t avail = written < L ? written : L;
+        const bool next_pre = ps + 1 < passes && 4 * (uint64_t)(p0 + 64 + t) < L;
+        have_pre = false;
+        auto prefetch = [&]() {
+            if (next_pre && !have_pre) load_inputs(p0 + 64, pre);
+            have_pre = next_pre;
+        };
+        while ((uint64_t)(done + 1) * 136 <= avail) {
+            uint64_t w[17];
+            load_block(w, 17);
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                a[i].lo ^= (uint32_t)w[i];
+                a[i].hi ^= (uint32_t)(w[i] >> 32);
+            }
+            prefetch();
+            perm<1>(a);
+            ++done;
+        }
+        prefetch();
+        __syncthreads();  // the next pass overwrites ring bytes this sweep has just absorbed
+    }
+    uint32_t dg[8];
+    {
+        // final (possibly empty) block: bytes [136 done, L) + FIPS-202 padding
+        const uint32_t rem = (uint32_t)(L - (uint64_t)done * 136);
+        uint64_t w[17];
+        load_block(w, (rem + 7) / 8);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            uint64_t v = 0;
+            if ((uint32_t)(8 * i) < rem) {
+                v = w[i];
+                const uint32_t left = rem - 8 * i;
+                if (left < 8) v &= ~0ull >> (64 - 8 * left);
+            }
+            a[i].lo ^= (uint32_t)v;
+            a[i].hi ^= (uint32_t)(v >> 32);
+        }
+        const uint32_t wi = rem >> 3, sh = (rem & 7) * 8;
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            if ((uint32_t)i == wi) {
+                if (sh < 32) a[i].lo ^= 0x06u << sh;
+                else a[i].hi ^= 0x06u << (sh - 32);
+            }
+        }
+        a[16].hi ^= 0x80000000u;
+        perm<1>(a);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            dg[2 * i] = a[i].lo;
+            dg[2 * i + 1] = a[i].hi;
+        }
+    }
+    uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)NODES * 32);
+    __syncthreads();  // the tree reuses the ring
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tree[t * 8 + i] = dg[i];
+    gout[2 * t] = make_uint4(dg[0], dg[1], dg[2], dg[3]);
+    gout[2 * t + 1] = make_uint4(dg[4], dg[5], dg[6], dg[7]);
+    __syncthreads();
+    uint32_t lbase = 0, cnt = N;
+    while (cnt > 1) {
+        const uint32_t nn = (cnt + 1) / 2;
+        if (t < nn) {
+            uint32_t h[8];
+            if (2 * t + 1 < cnt) {
+                uint32_t l[8], rr[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    l[i] = tree[(lbase + 2 * t) * 8 + i];
+                    rr[i] = tree[(lbase + 2 * t + 1) * 8 + i];
+                }
+                sha3_pair<1>(l, rr, h);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) h[i] = tree[(lbase + 2 * t) * 8 + i];
+            }
+            const uint32_t at = lbase + cnt + t;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tree[at * 8 + i] = h[i];
+            gout[2 * at] = make_uint4(h[0], h[1], h[2], h[3]);
+            gout[2 * at + 1] = make_uint4(h[4], h[5], h[6], h[7]);
+        }
+        __syncthreads();
+        lbase += cnt;
+        cnt = nn;
+    }
+}
+
 // Proof::validate(N) — one work-item per proof.
 __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len, const uint8_t* __restrict__ values,
                                                        uint64_t vstride, const uint32_t* __restrict__ index,
@@ -1047,6 +1317,18 @@ hipError_t launch_rbc_encode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uin
     if (D == 22 && Q == 42) return launch_fused<22, 42>(shards, S, L, n, payloads, pstride, plen, levels, st);
     if (D == 44 && Q == 84) return launch_fused<44, 84>(shards, S, L, n, payloads, pstride, plen, levels, st);
     return hipErrorInvalidValue;
+}
+
+bool has_fused_decoder(uint32_t D, uint32_t Q) { return D == 22 && Q == 42; }
+
+hipError_t launch_rbc_decode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
+                                    const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
+                                    uint8_t* levels, hipStream_t st) {
+    if (!(D == 22 && Q == 42)) return hipErrorInvalidValue;
+    HBG_GRID_CHECK(n, 64);
+    rbc_decode_merkle<22, 42><<<dim3((uint32_t)n), dim3(64), 0, st>>>(shards, S, L, n, present, plans, plan_stride,
+                                                                    levels);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,

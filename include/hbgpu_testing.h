@@ -33,11 +33,17 @@ int hbg_test_set_rbc_fused(hbg_ctx *ctx, int on);
  * one pass of the run-time coder; -1 (the default) 1 where Q > 16, where it
  * measured faster on MI355X.  Identical shards. */
 int hbg_test_set_rs_split(hbg_ctx *ctx, int on);
+/* Choose the schedule of hbg_rbc_decode: 0 rs_plan -> run-time coder (->
+ * constant parity encoder, per hbg_test_set_rs_split) -> merkle_build; 1 or
+ * -1 (the default) the single-launch rbc_decode_merkle kernel (reconstruct +
+ * Merkle rebuild, the missing rows transposed through LDS) where it exists —
+ * (D, Q) = (22, 42), N = 64 — and the three-launch schedule elsewhere.
+ * Identical shards, levels, statuses and payloads. */
+int hbg_test_set_rbc_decode_fused(hbg_ctx *ctx, int on);
 /* The BLS12-381 kernels exist in two builds with identical results: the
- * throughput build (serial multiply-accumulate chain per Fp multiplication
- * column, two waves per SIMD) and the latency build (three interleaved chains
- * and one wave per SIMD's register budget: fewer dependent stalls and spills
- * for a lone wave).  Launches of at most `lanes` work-items take the latency
+ * throughput build (G1 kernels at two waves per SIMD, pairing / G2 kernels at
+ * one) and the latency build (every kernel at one wave per SIMD's register
+ * budget: fewer dependent stalls and spills for a lone wave).  Launches of at most `lanes` work-items take the latency
  * build (default 65,536 = one wave per SIMD; 0: never; UINT64_MAX: always).
  * Process-wide; returns the previous value. */
 uint64_t hbg_test_set_latency_lanes(uint64_t lanes);

@@ -492,3 +492,68 @@ def test_batch_larger_than_one_grid_is_an_argument_error():
         assert bool((out[:, :8] != 0).any())
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("P,n", [(1 << 20, 10), (5000, 10), (0, 10), (47, 10)])
+def test_fused_decode_matches_three_launch_decode(P, n):
+    """hbg_test_set_rbc_decode_fused: the single-launch rbc_decode_merkle
+    (reconstruct + Merkle rebuild at N = 64) gives the same rebuilt shards,
+    statuses, lengths and payloads as rs_plan -> coders -> merkle_build, and
+    the oracle's decode, for: exactly 2f erased, only parity rows erased, every
+    data row erased, nothing erased, too few present, a wrong root, and a
+    corrupted present row past the first D (kept as received: None)."""
+    torch = _torch()
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    N = 64
+    pay, shards, levels, L, S = _device_batch(N, P, n, first=900)
+    data, parity = bc.shard_counts(N)
+    nodes = levels.shape[1]
+    pm = np.stack([synth.erasure_mask(900 + k, N, parity) for k in range(n)]).astype(np.uint8)
+    pm[1] = 1
+    pm[1, data:] = 0                                # only parity rows erased (42)
+    pm[2] = 1
+    pm[2, :data] = 0                                # every data row erased (22)
+    pm[3] = 1                                       # nothing erased
+    pm[4] = synth.erasure_mask(904, N, parity + 1)  # too few present -> None
+    pm[6] = synth.erasure_mask(906, N, parity - 5)
+    last = int(np.flatnonzero(pm[6])[-1])
+    present = torch.from_numpy(pm).to("cuda:0")
+    roots = levels[:, nodes - 1, :].contiguous()
+    roots[5, 3] ^= 0x40                             # wrong root -> None
+    base = shards.clone()
+    base[6, last, 0] ^= 0xFF                        # corrupted row past the first D: kept, root differs
+    OS = (data * L + 15) // 16 * 16
+    res = []
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        for fused in (0, 1):
+            _lib.check(_lib.lib().hbg_test_set_rbc_decode_fused(ctx.h, fused))
+            dmg = base.clone()
+            dmg[present == 0] = 0x5A
+            out = torch.zeros((n, OS), dtype=torch.uint8, device="cuda:0")
+            plen = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+            st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+            bc.rbc_decode_batch(N, L, dmg, present, roots, out, plen, st, ctx=ctx, device=True)
+            torch.cuda.synchronize()
+            res.append((dmg.cpu().numpy(), out.cpu().numpy(), plen.cpu().tolist(), st.cpu().tolist()))
+    finally:
+        ctx.close()
+    (d0, o0, l0, s0), (d1, o1, l1, s1) = res
+    assert s0 == s1 and l0 == l1
+    assert s1 == [1, 1, 1, 1, 0, 0, 0] + [1] * (n - 7)
+    ok = [k for k in range(n) if s1[k] == 1]
+    assert np.array_equal(d0[ok, :, :L], d1[ok, :, :L])     # rebuilt rows (rse: present rows as received)
+    for k in ok:
+        assert np.array_equal(o0[k, :l1[k]], o1[k, :l1[k]])
+        assert o1[k, :P].tobytes() == synth.payload(900 + k, P), k
+        assert np.array_equal(d1[k, :, :L], shards[k, :, :L].cpu().numpy()), k
+    # the oracle's decode_from_shards (C restatement) on a sampled instance of each kind
+    host = base.cpu().numpy()
+    for k in (0, 2, 6):
+        sh = np.ascontiguousarray(host[k, :, :L]).copy()
+        ref = corc.rbc_decode(N, L, sh, pm[k].copy(), roots[k].cpu().numpy().tobytes())
+        assert (ref is None) == (s1[k] == 0), k
+        if ref is not None:
+            assert o1[k, :len(ref)].tobytes() == ref, k

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--nodes", type=int, default=64)
     ap.add_argument("--payload", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--dec-fused", default="-1",
+                    help="decode schedules to time (hbg_test_set_rbc_decode_fused): 0 three launches, 1 fused")
     ap.add_argument("--splits", default="0,1",
                     help="decode schedules to time (hbg_test_set_rs_split): 0 one-pass, 1 data rows + constant "
                          "parity encoder, -1 the library default")
@@ -92,12 +94,18 @@ def main():
             out = torch.empty((B, OS), dtype=torch.uint8, device=dev)
             dpl = torch.empty(B, dtype=torch.int64, device=dev)
             dst = torch.empty(B, dtype=torch.uint8, device=dev)
-            for split in [int(x) for x in a.splits.split(",")]:  # hbg_test_set_rs_split
-                _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, split))
-                res[f"decode_split{split}_ms"] = t(lambda: bc.rbc_decode_batch(
-                    N, L, shards, present, roots, out, dpl, dst, ctx=ctx, device=True, asynchronous=True))
-                res[f"decode_split{split}_ok"] = bool((dst == 1).all().item())
+            for fz in [int(x) for x in a.dec_fused.split(",")]:  # hbg_test_set_rbc_decode_fused
+                _lib.check(_lib.lib().hbg_test_set_rbc_decode_fused(ctx.h, fz))
+                for split in [int(x) for x in a.splits.split(",")]:  # hbg_test_set_rs_split
+                    if fz != 0 and split != -1:
+                        continue  # the fused decoder has one schedule
+                    _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, split))
+                    res[f"decode_fused{fz}_split{split}_ms"] = t(lambda: bc.rbc_decode_batch(
+                        N, L, shards, present, roots, out, dpl, dst, ctx=ctx, device=True, asynchronous=True))
+                    res[f"decode_fused{fz}_split{split}_ok"] = bool((dst == 1).all().item()) and bool(
+                        torch.equal(out[:, :P], pay[:, :P]))
             _lib.check(_lib.lib().hbg_test_set_rs_split(ctx.h, -1))
+            _lib.check(_lib.lib().hbg_test_set_rbc_decode_fused(ctx.h, -1))
         print(json.dumps(res), flush=True)
         del pay, shards, levels
         torch.cuda.empty_cache()
