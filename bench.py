@@ -124,14 +124,16 @@ def pmc_traffic(instances: int) -> dict:
     return out
 
 
-# Kernels of one hbg_rbc_decode call at N = 64 (PMC passes: tools/gpu_r04a.sh,
-# profiles/r04/pmc_decode_8192.json; FETCH_SIZE x2 + WRITE_SIZE per kernel).
+# Kernels of one hbg_rbc_decode call at N = 64 (PMC passes: tools/gpu_r04d.sh /
+# gpu_r04g.sh on the default fused schedule, profiles/r04/pmc_decode_fused_8192.json;
+# FETCH_SIZE x2 + WRITE_SIZE per kernel; the three-launch schedule's passes are
+# profiles/r04/pmc_decode_8192.json).
 DECODE_KERNELS = ("rs_plan", "rs_code_movrel", "rs_encode_missing", "merkle_build", "rbc_glue_status",
                   "rbc_glue_copy", "rbc_decode_merkle")
 
 
 def decode_pmc_traffic(instances: int) -> dict:
-    path = os.path.join(ROOT, "profiles", "r04", "pmc_decode_8192.json")
+    path = os.path.join(ROOT, "profiles", "r04", "pmc_decode_fused_8192.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):

@@ -259,15 +259,16 @@ int reconstruct_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* 
 // hbg_rbc_decode's reconstruct + Merkle rebuild in one kernel (rbc_decode_merkle,
 // after rs_plan's data-only plan); the plan status goes to status_dev.
 int decode_fused_device(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shards, uint64_t S,
-                        const uint8_t* present_dev, uint64_t n, int32_t* status_dev, uint8_t* levels) {
+                        const uint8_t* present_dev, uint64_t n, int32_t* status_dev, uint8_t* levels, uint8_t* out,
+                        uint64_t ostride) {
     uint8_t* mat = nullptr;
     HBG_CHECK(device_matrix(c, D, Q, &mat));
     const uint64_t ps = plan_stride(D, Q);
     void* plans = nullptr;
     HBG_CHECK(scratch(c, 11, ps * n, &plans));
     HBG_TRY(launch_rs_plan(present_dev, D, Q, D, n, mat, (uint8_t*)plans, ps, c->stream));
-    HBG_TRY(launch_rbc_decode_merkle(D, Q, shards, S, L, n, present_dev, (const uint8_t*)plans, ps, levels,
-                                     c->stream));
+    HBG_TRY(launch_rbc_decode_merkle(D, Q, shards, S, L, n, present_dev, (const uint8_t*)plans, ps, levels, out,
+                                     ostride, c->stream));
     HBG_TRY(hipMemcpy2DAsync(status_dev, sizeof(int32_t), plans, ps, sizeof(int32_t), n, hipMemcpyDeviceToDevice,
                              c->stream));
     return HBG_OK;
@@ -615,7 +616,7 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
         HBG_CHECK(scratch(c, 10, sizeof(int32_t) * n, &ds));
         const bool fused = Q && c->dec_fused != 0 && has_fused_decoder(D, Q) && const_encoder_fits(D, Q, S, 0, false);
         if (fused) {
-            HBG_CHECK(decode_fused_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds, (uint8_t*)dl));
+            HBG_CHECK(decode_fused_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds, (uint8_t*)dl, dout, dos));
         } else {
             if (Q) {
                 HBG_CHECK(reconstruct_device(c, D, Q, L, dsh, S, dpres, n, (int32_t*)ds));
@@ -626,7 +627,7 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
             HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream));
         }
         HBG_TRY(launch_rbc_glue(dsh, S, L, N, D, n, (const uint8_t*)dl, droots, (const int32_t*)ds, dplen, dstat, dout,
-                                dos, c->stream));
+                                dos, c->stream, !fused));
         return HBG_OK;
     };
     if (flags & HBG_DEVICE) {

@@ -63,8 +63,17 @@ __host__ __device__ constexpr uint32_t plan_qpad(uint32_t max_out) {
     return (max_out + kGenericTile - 1) / kGenericTile * kGenericTile;
 }
 
-inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
+// Compact form of the same coefficients for the fused decoder: per (input j,
+// output o) one u16 at [j * qpad + o] = lo-nibble table index | (16 + hi
+// nibble) << 8 (its 32-entry register table), so a column's indices for every
+// output row are 11 scalar dwords.
+__host__ __device__ constexpr uint64_t plan_nidx_at(uint32_t D, uint32_t max_out) {
     return plan_offs_at(D, max_out) + 8ull * D * plan_qpad(max_out);
+}
+__host__ __device__ constexpr uint32_t nib_idx_pair(uint32_t c) { return (c & 15u) | ((16u + (c >> 4)) << 8); }
+
+inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
+    return (plan_nidx_at(D, max_out) + 2ull * D * plan_qpad(max_out) + 15) & ~uint64_t(15);
 }
 
 bool has_const_encoder(uint32_t D, uint32_t Q);
@@ -93,11 +102,13 @@ hipError_t launch_rs_encode_missing(uint32_t D, uint32_t Q, uint8_t* shards, uin
                                     const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
                                     hipStream_t st);
 // Fused reconstruct + Merkle rebuild after a data-only plan (rs_plan max_row =
-// D): missing data rows, missing parity rows and the levels in one launch.
+// D): missing data rows, missing parity rows, the levels and (out != null) the
+// glued payload bytes [0, D*L - 4) of every decodable instance in one launch;
+// rbc_glue's status pass then needs no copy pass (launch_rbc_glue copy=false).
 bool has_fused_decoder(uint32_t D, uint32_t Q);
 hipError_t launch_rbc_decode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                     const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
-                                    uint8_t* levels, hipStream_t st);
+                                    uint8_t* levels, uint8_t* out, uint64_t ostride, hipStream_t st);
 hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
                                uint8_t* levels, hipStream_t st);
 hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
@@ -106,7 +117,7 @@ hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* value
                                   hipStream_t st);
 hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                            const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
-                           uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st);
+                           uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st, bool copy = true);
 hipError_t launch_rbc_write_proof_msgs(uint32_t N, uint64_t L, const uint8_t* shards, uint64_t S,
                                        const uint8_t* levels, uint64_t n, uint32_t tag, uint64_t m,
                                        const uint64_t* inst, const uint32_t* index, uint8_t* out,

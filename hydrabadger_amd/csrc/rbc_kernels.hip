@@ -419,6 +419,7 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
     CodePlan* plan = reinterpret_cast<CodePlan*>(plans + inst * plan_stride);
     uint8_t* coef = reinterpret_cast<uint8_t*>(plan) + sizeof(CodePlan);
     uint32_t* offs = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(plan) + plan_offs_at(D, Q));
+    uint16_t* nidx = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(plan) + plan_nidx_at(D, Q));
     const uint32_t qp = plan_qpad(Q);
     const uint32_t t = threadIdx.x;
     // GF tables into LDS
@@ -441,6 +442,10 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
     __syncthreads();
     auto gmul = [&](uint32_t a, uint32_t b) -> uint32_t { return (a && b) ? ex[lg[a] + lg[b]] : 0u; };
     if (s_status != 0 || s_nout == 0) {
+        // nothing to rebuild below max_row: the input rows are still the plan's
+        // (rbc_decode_merkle re-encodes missing parity rows from them)
+        if (s_status == 0)
+            for (uint32_t j = t; j < D; j += blockDim.x) plan->in_idx[j] = (uint8_t)s_rows[j];
         if (t == 0) {
             plan->status = s_status ? -(int32_t)s_status : 0;
             plan->n_out = 0;
@@ -501,11 +506,13 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
         coef[o * D + c] = (uint8_t)acc;
         offs[2 * (c * qp + o)] = nib_off_lo(acc);
         offs[2 * (c * qp + o) + 1] = nib_off_hi(acc);
+        nidx[c * qp + o] = (uint16_t)nib_idx_pair(acc);
     }
     for (uint32_t e = t; e < (qp - no) * D; e += blockDim.x) {  // padding rows: the zero entries
         const uint32_t o = no + e / D, c = e % D;
         offs[2 * (c * qp + o)] = nib_off_lo(0);
         offs[2 * (c * qp + o) + 1] = nib_off_hi(0);
+        nidx[c * qp + o] = (uint16_t)nib_idx_pair(0);
     }
     for (uint32_t j = t; j < D; j += blockDim.x) plan->in_idx[j] = (uint8_t)s_rows[j];
     for (uint32_t o = t; o < no; o += blockDim.x) plan->out_idx[o] = s_out[o];
@@ -853,13 +860,14 @@ template <int D, int Q>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint64_t n,
                        const uint8_t* __restrict__ present, const uint8_t* __restrict__ plans, uint64_t plan_stride,
-                       uint8_t* __restrict__ levels) {
+                       uint8_t* __restrict__ levels, uint8_t* __restrict__ out, uint64_t ostride) {
     static_assert(D + Q == 64, "one wave per instance, lane = row");
     constexpr uint32_t N = D + Q, NODES = merkle_nodes(N);
     constexpr uint32_t R = fused_ring_bytes(4 * 64);
     typedef const __attribute__((address_space(4))) uint32_t* cu32;  // scalar (SMEM) loads
     typedef uint32_t v32 __attribute__((ext_vector_type(32)));      // dynamic uniform index -> v_movrels
     __shared__ __attribute__((aligned(16))) uint64_t lds[(Q * R > NODES * 32 ? Q * R : NODES * 32) / 8];
+    __shared__ uint32_t junk[64];  // landing area of the L2-warming loads (never read)
     uint32_t* ring = reinterpret_cast<uint32_t*>(lds);
     uint32_t* tree = reinterpret_cast<uint32_t*>(lds);
     const uint32_t t = threadIdx.x;
@@ -871,11 +879,19 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     const uint32_t n_out = __builtin_amdgcn_readfirstlane(plan->n_out);
     const uint64_t miss = __ballot(present[inst * N + t] == 0);      // bit r: row r is missing
     const uint64_t miss_data = miss & ((1ull << D) - 1ull);
+    // present rows past the first D present ones (the coding inputs): the
+    // absorb reads them straight from HBM, so each pass first pulls its 256-B
+    // window of them into L2 (buffer -> LDS loads into `junk`: no VGPR
+    // destination, nothing waits on them until the absorb)
+    uint64_t warm = ~miss;
+#pragma unroll
+    for (int j = 0; j < D; ++j) warm &= warm - 1ull;
     const uint64_t pres_data = ~miss & ((1ull << D) - 1ull);
     uint8_t* base = shards + inst * (uint64_t)N * S;
     const __amdgpu_buffer_rsrc_t rows = raw_rsrc(base);
+    const __amdgpu_buffer_rsrc_t orow = raw_rsrc(out ? out + inst * ostride : base);  // the glued payload
     const uint32_t qp = plan_qpad(Q);
-    const cu32 offs = (cu32)(pbase + plan_offs_at(D, Q));
+    const cu32 nidx = (cu32)(pbase + plan_nidx_at(D, Q));  // qp / 2 dwords per input column
     uint32_t in_off[D];  // byte offset of input row j (wave-uniform)
 #pragma unroll
     for (int j = 0; j < D; ++j) in_off[j] = __builtin_amdgcn_readfirstlane((uint32_t)plan->in_idx[j]) * (uint32_t)S;
@@ -918,6 +934,12 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         uint32_t wpos = (uint32_t)(((uint64_t)ps * 256) % R) + 4 * t;
         if (wpos >= R) wpos -= R;
         uint32_t* rcol = ring + wpos / 4;
+        for (uint64_t m = warm; m; m &= m - 1ull) {  // uniform loop, per-lane guard inside
+            const uint32_t r = (uint32_t)__builtin_ctzll(m);
+            const uint32_t so = __builtin_amdgcn_readfirstlane(r * (uint32_t)S + 4 * p0);
+            if (active)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rows, (__attribute__((address_space(3))) void*)junk, 4, 4 * t, so, 0, 0);
+        }
         if (active) {
             uint32_t win[D];
             if (have_pre) {
@@ -926,29 +948,33 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             } else {
                 load_inputs(p0, win);
             }
-            // ---- missing data rows: run-time coefficients over the D inputs
-            v32 acc;
+
+            // ---- missing data rows: run-time coefficients over the D inputs.
+            // The accumulators are plain registers (static indices); the one
+            // 32-entry table of an input word (lo nibbles 0..15, hi 16..31, the
+            // plan's offsets index it directly) is the only dynamically indexed
+            // vector, so the group branches below merge scalars, not vectors.
+            uint32_t acc[D];
 #pragma unroll
-            for (int o = 0; o < 32; ++o) acc[o] = 0u;
-            v32 wv;
-#pragma unroll
-            for (int j = 0; j < D; ++j) wv[j] = win[j];
-#pragma unroll
-            for (int j = D; j < 32; ++j) wv[j] = 0u;
+            for (int o = 0; o < D; ++o) acc[o] = 0u;
             if (n_out) {
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
                     uint32_t wj = win[j];
                     asm volatile("" : "+v"(wj));
                     const NibPair T = nib_tables(wj);
-                    typedef uint32_t v16 __attribute__((ext_vector_type(16)));
-                    v16 tl, th;
+                    v32 tab;
 #pragma unroll
                     for (int e = 0; e < 16; ++e) {
-                        tl[e] = T.lo.t[e];
-                        th[e] = T.hi.t[e];
+                        tab[e] = T.lo.t[e];
+                        tab[16 + e] = T.hi.t[e];
                     }
-                    const cu32 oj = offs + 2 * (uint64_t)j * qp;
+                    // the column's index pairs for every output row, loaded up front
+                    // (unconditional scalar loads: their latency hides under the table build)
+                    const cu32 nj = nidx + (uint64_t)j * (qp / 2);
+                    uint32_t ix[(D + 1) / 2];
+#pragma unroll
+                    for (int i = 0; i < (D + 1) / 2; ++i) ix[i] = nj[i];
                     // rows in groups of 4, a group only while o0 < n_out (wave-uniform);
                     // rows o >= n_out inside a group point at the zero entries (rs_plan's padding)
 #pragma unroll
@@ -956,8 +982,8 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                         if ((uint32_t)o0 < n_out) {
 #pragma unroll
                             for (int o = o0; o < (o0 + 4 < D ? o0 + 4 : D); ++o) {
-                                const uint32_t lo = oj[2 * o] >> 8, hi = (oj[2 * o + 1] >> 8) - 16u;
-                                acc[o] = xor3u(acc[o], tl[lo & 15u], th[hi & 15u]);
+                                const uint32_t pr = ix[o / 2] >> (16 * (o & 1));
+                                acc[o] = xor3u(acc[o], tab[pr & 31u], tab[(pr >> 8) & 31u]);
                             }
                         }
                     }
@@ -965,18 +991,41 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                     for (int o = 0; o < D; ++o) asm volatile("" : "+v"(acc[o]));
                 }
             }
-            // ---- the instance's data words: present -> its input word, missing -> rebuilt
+            v32 accv, winv;
+#pragma unroll
+            for (int o = 0; o < 32; ++o) {
+                accv[o] = o < D ? acc[o] : 0u;
+                winv[o] = o < D ? win[o] : 0u;
+            }
+            // ---- the instance's data words: present -> its input word, missing -> rebuilt;
+            // every data word also goes to the glued payload (value byte 4 on)
+            const bool tail_pass = 4 * (uint64_t)(p0 + 64) > L;  // this pass holds the rows' last word
             uint32_t d[D];
 #pragma unroll
             for (int J = 0; J < D; ++J) {
                 const uint32_t below = (uint32_t)((1ull << J) - 1ull);
                 if ((miss_data >> J) & 1ull) {
-                    const uint32_t o = (uint32_t)__builtin_popcountll(miss_data & below);
-                    d[J] = acc[o];
+                    d[J] = accv[(uint32_t)__builtin_popcountll(miss_data & below) & 31u];
                     __builtin_amdgcn_raw_buffer_store_b32(d[J], rows, 4 * t, J * (uint32_t)S + 4 * p0, 0);
                     rcol[slot_of(J) * (R / 4)] = d[J];
                 } else {
-                    d[J] = wv[(uint32_t)__builtin_popcountll(pres_data & below)];
+                    d[J] = winv[(uint32_t)__builtin_popcountll(pres_data & below) & 31u];
+                }
+                if (out) {
+                    // payload byte J*L + 4p - 4 (row 0's first word is the length
+                    // prefix: offset 2^32 - 4 lies past the resource, the store is
+                    // dropped).  Unaligned dword stores; the last word of a row
+                    // stores only its bytes below L, since the bytes past it are
+                    // the next row's, written in the first pass.
+                    const uint32_t vo = 4 * p + (uint32_t)J * (uint32_t)L - 4u;
+                    if (!tail_pass || 4 * (uint64_t)p + 4 <= L) {
+                        __builtin_amdgcn_raw_buffer_store_b32(d[J], orow, vo, 0, 0);
+                    } else {
+#pragma unroll
+                        for (uint32_t b = 0; b < 3; ++b)
+                            if (4 * (uint64_t)p + b < L)
+                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d[J] >> (8 * b)), orow, vo + b, 0, 0);
+                    }
                 }
             }
             // ---- parity: the compile-time encoder over the data words; missing rows stored
@@ -1323,11 +1372,11 @@ bool has_fused_decoder(uint32_t D, uint32_t Q) { return D == 22 && Q == 42; }
 
 hipError_t launch_rbc_decode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                     const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
-                                    uint8_t* levels, hipStream_t st) {
+                                    uint8_t* levels, uint8_t* out, uint64_t ostride, hipStream_t st) {
     if (!(D == 22 && Q == 42)) return hipErrorInvalidValue;
     HBG_GRID_CHECK(n, 64);
     rbc_decode_merkle<22, 42><<<dim3((uint32_t)n), dim3(64), 0, st>>>(shards, S, L, n, present, plans, plan_stride,
-                                                                    levels);
+                                                                    levels, out, ostride);
     return hipGetLastError();
 }
 
@@ -1382,7 +1431,7 @@ hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* value
 
 hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                            const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
-                           uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st) {
+                           uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st, bool copy) {
     const uint32_t nodes = merkle_nodes(N);
     const uint64_t maxlen = (uint64_t)D * L;
     const uint32_t bpi = (uint32_t)(((maxlen + 15) / 16 + 255) / 256);
@@ -1390,7 +1439,7 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
     rbc_glue_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(shards, S, L, N, D, n, levels, nodes,
                                                                             roots, rstatus, plen, status);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || !copy) return e;
     rbc_glue_copy<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, plen, status, out,
                                                                     ostride);
     return hipGetLastError();

@@ -160,7 +160,11 @@ int hbg_rbc_encode_merkle(hbg_ctx *ctx, uint32_t N, const uint8_t *payloads,
 /* decode_from_shards + glue_shards (a7+a8): reconstruct in place, rebuild the
  * tree over all N shards, compare with roots[k]; on match glue the first
  * data shards: payload_out + k*payload_stride gets payload_len[k] bytes and
- * status[k] = HBG_DECODE_OK, else status[k] = HBG_DECODE_NONE. */
+ * status[k] = HBG_DECODE_OK, else status[k] = HBG_DECODE_NONE.
+ * payload_stride >= D * shard_len (D = N - 2f data shards).  Bytes of a
+ * payload row past payload_len[k], and the whole row of a NONE instance, are
+ * unspecified (the fused N = 64 decoder writes the glued bytes while it
+ * rebuilds, before the root comparison). */
 int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards,
                    uint64_t shard_stride, const uint8_t *present, const uint8_t *roots,
                    uint8_t *payload_out, uint64_t payload_stride, uint64_t *payload_len,

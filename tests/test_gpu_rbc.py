@@ -243,10 +243,11 @@ def _device_batch(N, P, n, first=0):
     from hydrabadger_amd import _lib
     L = _lib.shard_len(N, P)
     S = (L + 15) // 16 * 16
-    PS = (P + 15) // 16 * 16
+    PS = max(16, (P + 15) // 16 * 16)
     dev = torch.device("cuda:0")
-    pay = torch.empty((n, PS), dtype=torch.uint8, device=dev)
-    bc.synth_bytes(synth.TAG_PAYLOAD, first, P, pay, device=True)
+    pay = torch.zeros((n, PS), dtype=torch.uint8, device=dev)
+    if P:
+        bc.synth_bytes(synth.TAG_PAYLOAD, first, P, pay, device=True)
     plen = torch.full((n,), P, dtype=torch.int64, device=dev)
     shards = torch.empty((n, N, S), dtype=torch.uint8, device=dev)
     levels = torch.empty((n, _lib.merkle_nodes(N), 32), dtype=torch.uint8, device=dev)

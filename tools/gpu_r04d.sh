@@ -35,9 +35,7 @@ for k, v in d.items():
         print(k[:40], round(v["avg_ms"], 2), "ms read", round(v.get("hbm_read_bytes_corrected", 0) / 1e9, 2),
               "GB write", round(v.get("hbm_write_bytes", 0) / 1e9, 2), "GB valu/wave", round(v.get("valu_insts_per_wave", 0)))
 PY
-echo "== fp subroutine issue rate"
-timeout -k 10 120 ./tools/ubench6 > "$OUT/ubench6.json" 2>&1 || { cat "$OUT/ubench6.json"; exit 7; }
-cat "$OUT/ubench6.json"
+[ -n "${SKIP_SUITE:-}" ] && { echo "== done (suite skipped)"; exit 0; }
 echo "== full GPU suite"
 timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
     > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 5; }
