@@ -74,6 +74,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
 }
 constexpr int kBufSc1 = 16;  // buffer aux bit: sc1 (served by L2, not the CU's vector L1)
+// Cache policy of the encode / decode kernels' row, payload and level stores
+// (buffer aux: 2 = nt, streamed past L2 so they do not evict the rows the
+// absorb re-reads; 0 = default).
+#ifndef HBG_STORE_AUX
+#define HBG_STORE_AUX 2
+#endif
+constexpr int kStoreAux = HBG_STORE_AUX;
 
 // The rows of one encode: shard rows through `sh` (row J of the instance at
 // byte J*S + vsh of the resource; vsh = the lane's instance offset + 4t) and
@@ -134,7 +141,7 @@ struct EncodeCtx {
             w = buf[J % kPrefetch].x;
         }
         if constexpr (MODE != 0)
-            __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), 0);
+            __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), kStoreAux);
         return w;
     }
 
@@ -181,7 +188,8 @@ __device__ __forceinline__ void encode_word(const EncodeRows& r) {
         if constexpr (MASKED) {
             if (!(((k < 64) ? (r.miss0 >> k) : (r.miss1 >> (k & 63))) & 1u)) continue;
         }
-        __builtin_amdgcn_raw_buffer_store_b32(acc[k], r.sh, r.vsh, (uint32_t)((uint64_t)(D + k) * r.S + 4 * r.p0), 0);
+        __builtin_amdgcn_raw_buffer_store_b32(acc[k], r.sh, r.vsh, (uint32_t)((uint64_t)(D + k) * r.S + 4 * r.p0),
+                                              kStoreAux);
         if constexpr (RING) r.ring[k * r.rdw] = acc[k];
     }
 }
@@ -1006,7 +1014,7 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                 const uint32_t below = (uint32_t)((1ull << J) - 1ull);
                 if ((miss_data >> J) & 1ull) {
                     d[J] = accv[(uint32_t)__builtin_popcountll(miss_data & below) & 31u];
-                    __builtin_amdgcn_raw_buffer_store_b32(d[J], rows, 4 * t, J * (uint32_t)S + 4 * p0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(d[J], rows, 4 * t, J * (uint32_t)S + 4 * p0, kStoreAux);
                     rcol[slot_of(J) * (R / 4)] = d[J];
                 } else {
                     d[J] = winv[(uint32_t)__builtin_popcountll(pres_data & below) & 31u];
@@ -1019,12 +1027,13 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                     // the next row's, written in the first pass.
                     const uint32_t vo = 4 * p + (uint32_t)J * (uint32_t)L - 4u;
                     if (!tail_pass || 4 * (uint64_t)p + 4 <= L) {
-                        __builtin_amdgcn_raw_buffer_store_b32(d[J], orow, vo, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(d[J], orow, vo, 0, kStoreAux);
                     } else {
 #pragma unroll
                         for (uint32_t b = 0; b < 3; ++b)
                             if (4 * (uint64_t)p + b < L)
-                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d[J] >> (8 * b)), orow, vo + b, 0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d[J] >> (8 * b)), orow, vo + b, 0,
+                                                                     kStoreAux);
                     }
                 }
             }
@@ -1045,7 +1054,8 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
 #pragma unroll
             for (int k = 0; k < Q; ++k) {
                 if ((miss >> (D + k)) & 1ull) {
-                    __builtin_amdgcn_raw_buffer_store_b32(accp[k], rows, 4 * t, (D + k) * (uint32_t)S + 4 * p0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(accp[k], rows, 4 * t, (D + k) * (uint32_t)S + 4 * p0,
+                                                          kStoreAux);
                     rcol[slot_of(D + k) * (R / 4)] = accp[k];
                 }
             }

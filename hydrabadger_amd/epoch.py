@@ -69,7 +69,7 @@ from . import _lib
 from . import broadcast as bc
 from . import tdec_workload as tw
 from .network import all_gather_rows, all_to_all_bytes, proof_index_map
-from .workload import SplitMix64
+from .workload import BASE_SEED, GAMMA, SplitMix64
 
 TAG_CONTRIB, TAG_R, TAG_ARRIVAL = 6, 7, 8
 CT_HEAD, CT_TAIL = 48 + 8, 96
@@ -93,12 +93,31 @@ def arrival_orders(epoch: int, proposers, n: int, node: int = -1) -> np.ndarray:
     """[k][n] senders of instance proposers[k]'s decryption shares in arrival
     order at `node` (-1: the shared view) — a seeded permutation: the
     network's timing, an input."""
-    out = np.zeros((len(proposers), n), np.int64)
-    for k, p in enumerate(proposers):
-        rng = SplitMix64(TAG_ARRIVAL, arrival_id(epoch, int(p), node))
-        keys = [rng.next() for _ in range(n)]
-        out[k] = sorted(range(n), key=lambda s: (keys[s], s))
-    return out
+    return arrival_orders_views(epoch, proposers, n, [node])[0]
+
+
+def _i64(x: int) -> int:
+    """A u64 constant as the int64 with the same bits (torch arithmetic wraps)."""
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def arrival_orders_views(epoch: int, proposers, n: int, nodes, device=None) -> np.ndarray:
+    """[len(nodes)][k][n]: arrival_orders for several views at once — the
+    same SplitMix64 streams (sender s's key = the stream's (s+1)-th output,
+    ties by sender), evaluated as wrapping 64-bit tensor arithmetic (on
+    `device` when given) instead of one Python call per key (a 128-node epoch
+    has 128 x 128 x 128 keys)."""
+    ids = [[arrival_id(epoch, int(p), int(v)) ^ BASE_SEED ^ (TAG_ARRIVAL << 48) for p in proposers] for v in nodes]
+    seed = torch.tensor([[_i64(x) for x in row] for row in ids], dtype=torch.int64, device=device)   # [v][k]
+    z = seed.unsqueeze(-1) + _i64(GAMMA) * torch.arange(1, n + 1, dtype=torch.int64, device=device)
+
+    def shr(x, k):  # logical shift of the u64 bits
+        return (x >> k) & ((1 << (64 - k)) - 1)
+    z = (z ^ shr(z, 30)) * _i64(0xBF58476D1CE4E5B9)
+    z = (z ^ shr(z, 27)) * _i64(0x94D049BB133111EB)
+    z = z ^ shr(z, 31)
+    key = z ^ (-(1 << 63))  # u64 order as int64 order
+    return torch.sort(key, dim=-1, stable=True).indices.cpu().numpy().astype(np.int64)
 
 
 @dataclass(frozen=True)
@@ -220,13 +239,13 @@ class HoneyBadgerEpoch:
         return value_ok, vrecv, run_off, len(g_len)
 
     def run(self, epoch: int = 0, faults: Faults = Faults(), per_node: bool = True,
-            decode_chunk: int = 8) -> EpochResult:
+            decode_chunk: int = 32, echo_chunk: int = 32) -> EpochResult:
         """One epoch.  per_node: every local node does its own work (Values
         addressed to it, all echoes, its decodes, its ThresholdDecrypt of every
         accepted ciphertext with its own arrival order); otherwise the shared
         view (one check / decode / TDec instance per rank on behalf of all
-        its nodes).  decode_chunk: local nodes whose decode copies are
-        resident at once."""
+        its nodes).  decode_chunk / echo_chunk: local nodes whose decode
+        copies / echo tables are resident (and launched) at once."""
         e, N, m, L, C, P, f = self.engine, self.N, self.m, self.L, self.C, self.P, self.f
         dev = e.device
         r0 = self.rank * m
@@ -291,8 +310,15 @@ class HoneyBadgerEpoch:
         tag, vals, idx, dig, nd, roots, st = e.read_msgs(N, L, eall, ge_off)
         s_of = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(N)
         parsed = (st == 0) & (tag == _lib.HBG_MSG_ECHO) & (idx == s_of)
-        # every view validates every echo it receives (hbbft handle_echo)
-        eok = [e.validate_table(N, L, vals, idx, dig, nd, roots) for _ in range(nv)]
+        # every view validates every echo it receives (hbbft handle_echo): each
+        # view its own copy of the N x N echoes, up to echo_chunk views per
+        # launch (one view's N*N proofs are too few lanes to fill the chip)
+        eok = []
+        for c0 in range(0, nv, echo_chunk):
+            c = min(echo_chunk, nv - c0)
+            rep = (lambda x: x.repeat(c, *([1] * (x.dim() - 1)))) if c > 1 else (lambda x: x)
+            okc = e.validate_table(N, L, rep(vals), rep(idx), rep(dig), rep(nd), rep(roots))
+            eok += list(okc.view(c, -1))
         work["echo_validations"] = nv * N * N
         echo_ok_v = torch.stack([(parsed & (x == 1)).view(N, N) & (esent_all == 1) for x in eok])   # [v][s][p]
         # echoes per root: the root with the most valid echoes (ties: lowest sender)
@@ -367,12 +393,12 @@ class HoneyBadgerEpoch:
             sall = self._gather(shares.permute(1, 0, 2).contiguous())   # [N s][k][48]
             share48 = sall.permute(1, 0, 2).contiguous()                # [k][N][48]
             silent = np.array([s in faults.silent for s in range(N)])
-            arr = np.full((nv, k, N), -1, np.int32)
-            for vi, node in enumerate(views):
-                order = arrival_orders(epoch, acc, N, node)
-                for q in range(k):
-                    o = order[q][~silent[order[q]]]
-                    arr[vi, q, :len(o)] = o
+            order = arrival_orders_views(epoch, acc, N, views, dev)         # [v][k][N]
+            keep = ~silent[order]
+            # silent senders' entries dropped, the rest kept in arrival order, -1 padded
+            order = np.take_along_axis(order, np.argsort(~keep, axis=-1, kind="stable"), -1)
+            order[np.arange(N) >= keep.sum(-1, keepdims=True)] = -1
+            arr = order.astype(np.int32)
             # view v's instance of ciphertext q: its own copy of (U, V, W) and the N shares
             V_off = torch.arange(nv * k + 1, dtype=torch.int64, device=dev) * P
             pt, ct_status, outcome = e.threshold_decrypt(

@@ -17,8 +17,8 @@ with X_k in v[24k, 24k+11], Y_k in v[24k+12, 24k+23] (12 x u32 LE limbs,
 Montgomery form, < p), R_k written over X_k.  Temporaries per slot k (base
 T = 24N): accumulator v[T+2k : T+2k+1], carry count v[T+2N+k], Montgomery
 quotients m_k[0..11] at v[T+3N+12k ..].  SGPRs: p limbs s[64:75], -p^-1 mod
-2^32 s76, carries s[78+2k : 79+2k], reduction mask s[84:85], call target
-s[86:87], return address s[30:31].  The N products run interleaved (product
+2^32 s76, carries s[78+2k : 79+2k] and s[88+2k : 89+2k] (alternating), reduction
+mask s[84:85], call target s[86:87], return address s[30:31].  The N products run interleaved (product
 scanning, one v_mad_u64_u32 + carry count per partial product): with N = 3
 a carry SGPR is read two instructions after its write, so no wait states are
 spent and a lone wave per SIMD still issues back to back (three independent
@@ -45,6 +45,7 @@ S_N0 = 76
 S_CARRY = 78    # s[78+2k : 79+2k]
 S_MASK = 84     # s[84:85]
 S_TGT = 86      # s[86:87] call target
+S_CARRY2 = 88   # s[88+2k : 89+2k]: the second carry set (partial products alternate sets)
 VALU_SGPR_WAIT = 2  # wait states between a VALU SGPR write and a VALU read of it
 
 
@@ -99,7 +100,7 @@ def regs(N):
         slots.append({
             "x": 24 * k, "y": 24 * k + 12,
             "acc": T + 2 * k, "t2": T + 2 * N + k, "m": T + 3 * N + 12 * k,
-            "sc": S_CARRY + 2 * k,
+            "sc": S_CARRY + 2 * k, "sc2": S_CARRY2 + 2 * k,
         })
     return slots, 39 * N
 
@@ -116,18 +117,38 @@ def gen_sub(N: int) -> str:
         e.valu(f"v_mov_b32 {v(s['t2'])}, 0")
 
     def mac(prods):
-        """prods: list of (xkind, xi, ykind, yi); kinds 'x' | 'y' | 'm' | 'p'."""
-        for (xk, xi, yk, yi) in prods:
+        """prods: list of (xkind, xi, ykind, yi); kinds 'x' | 'y' | 'm' | 'p'.
+
+        Software-pipelined carry counts: partial product q's carries go to
+        carry set q % 2 and are counted (v_addc into t2) after product q+1's
+        mads, so a carry SGPR is read 2N instructions after its write instead
+        of N (a lone wave's mad -> addc latency), and the two sets never
+        overlap.  The last product's counts are drained at the end."""
+        def carry(s, cs):
+            return s["sc"] if cs == 0 else s["sc2"]
+
+        def counts(cs):
+            for s in slots:
+                c = carry(s, cs)
+                e.valu(f"v_addc_co_u32_e64 {v(s['t2'])}, {sp(c)}, {v(s['t2'])}, 0, {sp(c)}",
+                       reads=(c,), writes=(c,))
+
+        pending = None
+        for q, (xk, xi, yk, yi) in enumerate(prods):
+            cs = q % 2
             for s in slots:
                 def op(kind, i):
                     if kind == "p":
                         return f"s{S_P + i}"
                     return v(s[kind] + i)
-                e.valu(f"v_mad_u64_u32 {vp(s['acc'])}, {sp(s['sc'])}, {op(xk, xi)}, {op(yk, yi)}, {vp(s['acc'])}",
-                       writes=(s["sc"],))
-            for s in slots:
-                e.valu(f"v_addc_co_u32_e64 {v(s['t2'])}, {sp(s['sc'])}, {v(s['t2'])}, 0, {sp(s['sc'])}",
-                       reads=(s["sc"],), writes=(s["sc"],))
+                c = carry(s, cs)
+                e.valu(f"v_mad_u64_u32 {vp(s['acc'])}, {sp(c)}, {op(xk, xi)}, {op(yk, yi)}, {vp(s['acc'])}",
+                       writes=(c,))
+            if pending is not None:
+                counts(pending)
+            pending = cs
+        if pending is not None:
+            counts(pending)
 
     for i in range(24):
         prods = []
@@ -181,7 +202,7 @@ def gen_sub(N: int) -> str:
 def clobbers(N: int, nv: int) -> str:
     # VGPRs the subroutine writes besides the outputs X_k: all temporaries
     vs = [f'"v{i}"' for i in range(24 * N, nv)]
-    ss = [f'"s{i}"' for i in range(S_P, S_TGT + 2)] + ['"s30"', '"s31"', '"scc"']
+    ss = [f'"s{i}"' for i in range(S_P, S_CARRY2 + 6)] + ['"s30"', '"s31"', '"scc"']
     return ", ".join(vs + ss)
 
 
