@@ -63,17 +63,19 @@ __host__ __device__ constexpr uint32_t plan_qpad(uint32_t max_out) {
     return (max_out + kGenericTile - 1) / kGenericTile * kGenericTile;
 }
 
-// Compact form of the same coefficients for the fused decoder: per (input j,
-// output o) one u16 at [j * qpad + o] = lo-nibble table index | (16 + hi
-// nibble) << 8 (its 32-entry register table), so a column's indices for every
-// output row are 11 scalar dwords.
+// Compact form of the same coefficients for the fused decoder (data-only
+// plans, n_out <= D): per (input j, output o < D2 = round_up(D, 2)) one u16 at
+// [j * D2 + o] = lo-nibble table index | (16 + hi nibble) << 8 (its 32-entry
+// register table), dense, so a column's indices are D2 / 2 scalar dwords and
+// an instance's whole table (22 x 11 dwords at N = 64) stays in the scalar cache.
+__host__ __device__ constexpr uint32_t plan_nidx_rows(uint32_t D) { return (D + 1) & ~1u; }
 __host__ __device__ constexpr uint64_t plan_nidx_at(uint32_t D, uint32_t max_out) {
     return plan_offs_at(D, max_out) + 8ull * D * plan_qpad(max_out);
 }
 __host__ __device__ constexpr uint32_t nib_idx_pair(uint32_t c) { return (c & 15u) | ((16u + (c >> 4)) << 8); }
 
 inline uint64_t plan_stride(uint32_t D, uint32_t max_out) {
-    return (plan_nidx_at(D, max_out) + 2ull * D * plan_qpad(max_out) + 15) & ~uint64_t(15);
+    return (plan_nidx_at(D, max_out) + 2ull * D * plan_nidx_rows(D) + 15) & ~uint64_t(15);
 }
 
 bool has_const_encoder(uint32_t D, uint32_t Q);

@@ -514,13 +514,13 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
         coef[o * D + c] = (uint8_t)acc;
         offs[2 * (c * qp + o)] = nib_off_lo(acc);
         offs[2 * (c * qp + o) + 1] = nib_off_hi(acc);
-        nidx[c * qp + o] = (uint16_t)nib_idx_pair(acc);
+        if (o < plan_nidx_rows(D)) nidx[c * plan_nidx_rows(D) + o] = (uint16_t)nib_idx_pair(acc);
     }
     for (uint32_t e = t; e < (qp - no) * D; e += blockDim.x) {  // padding rows: the zero entries
         const uint32_t o = no + e / D, c = e % D;
         offs[2 * (c * qp + o)] = nib_off_lo(0);
         offs[2 * (c * qp + o) + 1] = nib_off_hi(0);
-        nidx[c * qp + o] = (uint16_t)nib_idx_pair(0);
+        if (o < plan_nidx_rows(D)) nidx[c * plan_nidx_rows(D) + o] = (uint16_t)nib_idx_pair(0);
     }
     for (uint32_t j = t; j < D; j += blockDim.x) plan->in_idx[j] = (uint8_t)s_rows[j];
     for (uint32_t o = t; o < no; o += blockDim.x) plan->out_idx[o] = s_out[o];
@@ -899,7 +899,7 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     const __amdgpu_buffer_rsrc_t rows = raw_rsrc(base);
     const __amdgpu_buffer_rsrc_t orow = raw_rsrc(out ? out + inst * ostride : base);  // the glued payload
     const uint32_t qp = plan_qpad(Q);
-    const cu32 nidx = (cu32)(pbase + plan_nidx_at(D, Q));  // qp / 2 dwords per input column
+    const cu32 nidx = (cu32)(pbase + plan_nidx_at(D, Q));  // plan_nidx_rows(D) / 2 dwords per input column
     uint32_t in_off[D];  // byte offset of input row j (wave-uniform)
 #pragma unroll
     for (int j = 0; j < D; ++j) in_off[j] = __builtin_amdgcn_readfirstlane((uint32_t)plan->in_idx[j]) * (uint32_t)S;
@@ -913,9 +913,9 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     uint32_t done = 0;
     // words [0, nw) of the 136-byte block of row t at byte 136 * done (a
     // shard row is read only below round_up(L, 8) <= S)
-    auto load_block = [&](uint64_t (&w)[17], uint32_t nw) {
+    auto load_block = [&](uint64_t (&w)[17], uint32_t nw, uint32_t blk) {
         if (row_missing) {
-            const uint32_t rp = (136u * done) % R / 8;
+            const uint32_t rp = (136u * blk) % R / 8;
 #pragma unroll
             for (int i = 0; i < 17; ++i) w[i] = rrow[rp + i];
         } else {
@@ -923,7 +923,7 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             for (int i = 0; i < 17; ++i) {
                 w[i] = 0;
                 if ((uint32_t)i < nw) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rows, t * (uint32_t)S + 8 * i, 136 * done, 0);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rows, t * (uint32_t)S + 8 * i, 136 * blk, 0);
                     w[i] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
                 }
             }
@@ -979,7 +979,7 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                     }
                     // the column's index pairs for every output row, loaded up front
                     // (unconditional scalar loads: their latency hides under the table build)
-                    const cu32 nj = nidx + (uint64_t)j * (qp / 2);
+                    const cu32 nj = nidx + (uint64_t)j * (plan_nidx_rows(D) / 2);
                     uint32_t ix[(D + 1) / 2];
 #pragma unroll
                     for (int i = 0; i < (D + 1) / 2; ++i) ix[i] = nj[i];
@@ -1069,15 +1069,20 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             if (next_pre && !have_pre) load_inputs(p0 + 64, pre);
             have_pre = next_pre;
         };
+        // the next block of the same sweep is loaded before this block's
+        // permutation (its latency hides under it)
+        uint64_t w[17];
+        bool have_w = false;
         while ((uint64_t)(done + 1) * 136 <= avail) {
-            uint64_t w[17];
-            load_block(w, 17);
+            if (!have_w) load_block(w, 17, done);
 #pragma unroll
             for (int i = 0; i < 17; ++i) {
                 a[i].lo ^= (uint32_t)w[i];
                 a[i].hi ^= (uint32_t)(w[i] >> 32);
             }
             prefetch();
+            have_w = (uint64_t)(done + 2) * 136 <= avail;
+            if (have_w) load_block(w, 17, done + 1);
             perm<1>(a);
             ++done;
         }
@@ -1089,7 +1094,7 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         // final (possibly empty) block: bytes [136 done, L) + FIPS-202 padding
         const uint32_t rem = (uint32_t)(L - (uint64_t)done * 136);
         uint64_t w[17];
-        load_block(w, (rem + 7) / 8);
+        load_block(w, (rem + 7) / 8, done);
 #pragma unroll
         for (int i = 0; i < 17; ++i) {
             uint64_t v = 0;
@@ -1385,6 +1390,9 @@ hipError_t launch_rbc_decode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uin
                                     uint8_t* levels, uint8_t* out, uint64_t ostride, hipStream_t st) {
     if (!(D == 22 && Q == 42)) return hipErrorInvalidValue;
     HBG_GRID_CHECK(n, 64);
+#ifdef HBG_DEC_NO_PAYLOAD  // diagnostic variant (tools/build_variant.py): the payload stores left out
+    out = nullptr;
+#endif
     rbc_decode_merkle<22, 42><<<dim3((uint32_t)n), dim3(64), 0, st>>>(shards, S, L, n, present, plans, plan_stride,
                                                                     levels, out, ostride);
     return hipGetLastError();

@@ -190,10 +190,21 @@ __global__ __launch_bounds__(256) void tdec_keystream_xor(uint64_t n, const uint
                  ((uint32_t)sd[4 * i + 3] << 24);
     const uint64_t o = off[k], len = off[k + 1] - o;
     const uint64_t nb = (len + 15) / 16;
+    const bool vec = (((uintptr_t)(in + o) | (uintptr_t)(out + o)) & 15u) == 0;
     for (uint64_t c = threadIdx.x; c < nb; c += blockDim.x) {
         uint32_t w[16];
         chacha_block(key, (uint32_t)c, w);
         const uint64_t b0 = 16 * c;
+        if (vec && b0 + 16 <= len) {  // one 16-B load and store: the keystream is each word's low byte
+            uint32_t ks[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                ks[i] = __builtin_amdgcn_perm(w[4 * i + 1], w[4 * i], 0x0c0c0400u) |
+                        __builtin_amdgcn_perm(w[4 * i + 3], w[4 * i + 2], 0x04000c0cu);
+            const uint4 v = *reinterpret_cast<const uint4*>(in + o + b0);
+            *reinterpret_cast<uint4*>(out + o + b0) = make_uint4(v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3]);
+            continue;
+        }
 #pragma unroll
         for (int b = 0; b < 16; ++b)
             if (b0 + b < len) out[o + b0 + b] = in[o + b0 + b] ^ (uint8_t)(w[b] & 0xFFu);
