@@ -746,7 +746,7 @@ bool use_batched(const hbg_ctx* c, uint64_t n) {
 int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uint8_t* dU48, uint32_t n,
                           uint32_t n_pk, const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp,
                           const uint32_t* paff, const int32_t* pst, uint8_t* dok,
-                          const std::function<int()>& after_leaves = {}) {
+                          const std::function<int()>& after_leaves = {}, uint32_t* share_aff = nullptr) {
     uint32_t* tbl = nullptr;
     if (c->tdec_batched == 2 || (uint64_t)n >= kPkTableMinUses * n_pk) {
         void* p;
@@ -823,7 +823,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
 #endif
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.ct_status, paff, pst, tbl,
-                                          (uint32_t*)sums, (uint8_t*)lok, c->stream));
+                                          (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
     if (after_leaves) HBG_CHECK(after_leaves());
     // round 0: every batch sum; failing batches push their 16-share groups
@@ -1074,13 +1074,18 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_TRY(bls::launch_tdec_pair_index(n, n_nodes, sct, spk, c->stream));
     void *paff, *pst;
     HBG_CHECK(prepare_pks(c, n_nodes, (const uint8_t*)dpk, &paff, &pst));
+    // the verified shares' affine points, written by the verification and read
+    // by the combine (no second decompression of the t + 1 selected shares)
+    void* saff;
+    HBG_CHECK(scratch(c, 45, 4ull * bls::kAffWords * n, &saff));
     if (batched) {
         HBG_CHECK(verify_shares_batched(c, n_ct, tab, tab.U48, (uint32_t)n, n_nodes, (const uint8_t*)dsh, sct, spk,
-                                        (const uint32_t*)paff, (const int32_t*)pst, (uint8_t*)okb, ct_verify));
+                                        (const uint32_t*)paff, (const int32_t*)pst, (uint8_t*)okb, ct_verify,
+                                        (uint32_t*)saff));
     } else {
         HBG_TRY(bls::launch_tdec_verify_shares(n, nullptr, (const uint8_t*)dsh, sct, spk, tab.ct_u, tab.ct_status,
                                                tab.coefH, tab.coefW, (const uint32_t*)paff, (const int32_t*)pst,
-                                               (uint8_t*)okb, c->stream));
+                                               (uint8_t*)okb, c->stream, nullptr, (uint32_t*)saff));
     }
     HBG_CHECK(join_aux(c));  // ct_verify's verdicts are read by tdec_select
     // handle_message / try_output: the first t+1 valid arrivals, faults, late shares
@@ -1097,7 +1102,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_CHECK(scratch(c, 39, 4ull * 32 * m * n_ct, &scr));
     HBG_CHECK(scratch(c, 41, 32ull * n_ct, &sds));
     HBG_TRY(bls::launch_tdec_combine(n_ct, t, s48, sidx, dV, dVoff, (uint8_t*)dpt, (int32_t*)dst, (uint32_t*)scr,
-                                     (uint8_t*)sds, c->stream));
+                                     (uint8_t*)sds, c->stream, (const uint32_t*)saff, n_nodes, sst));
     HBG_TRY(bls::launch_tdec_status_merge(n_ct, sst, (int32_t*)dst, c->stream));
     return drain(c, flags, {{plaintext, {dpt, vlen}}, {status, {dst, 4ull * n_ct}}, {outcome, {doc, n}}});
 }

@@ -41,7 +41,7 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
                                      const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
                                      const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
                                      const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
-                                     const uint32_t* sel = nullptr);
+                                     const uint32_t* sel = nullptr, uint32_t* share_aff = nullptr);
 hipError_t launch_tdec_index_sanitize(uint64_t n, const uint32_t* a, uint32_t a_bound, const uint32_t* b,
                                       uint32_t b_bound, uint32_t* a_out, uint32_t* b_out, int32_t* err,
                                       hipStream_t st);
@@ -55,7 +55,7 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
                                     const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
-                                    uint8_t* leaf_ok, hipStream_t st);
+                                    uint8_t* leaf_ok, hipStream_t st, uint32_t* share_aff = nullptr);
 size_t tdec_pk_table_bytes(uint32_t n_pk);
 hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st);
 hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const CheckItem* items,
@@ -104,10 +104,16 @@ hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8
                               hipStream_t st);
 hipError_t launch_tdec_pair_index(uint64_t n, uint32_t N, uint32_t* sct, uint32_t* spk, hipStream_t st);
 hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32_t* status, hipStream_t st);
-// seeds: [n][32] scratch (xor_with_hash keys, consumed by tdec_keystream_xor)
+// seeds: [n][32] scratch (xor_with_hash keys, consumed by tdec_keystream_xor).
+// share_aff (nullable): the verified shares' affine points [n][n_nodes][kAffWords]
+// written by the share verification (leaves / verify_shares): the combine
+// reads share idx[i] of ciphertext g there instead of decompressing share48;
+// pre_status (nullable, with share_aff): a ciphertext whose selection failed
+// is skipped (its status is the selection's).
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
-                               uint32_t* scratch, uint8_t* seeds, hipStream_t st);
+                               uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff = nullptr,
+                               uint32_t n_nodes = 0, const int32_t* pre_status = nullptr);
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,
                             uint32_t out_words, uint32_t* lines, hipStream_t st);
 

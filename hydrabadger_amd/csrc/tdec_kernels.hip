@@ -743,16 +743,21 @@ __global__ __launch_bounds__(256) void tdec_status_or(uint32_t n, int32_t* __res
     if (k < n && status[k] == 0) status[k] = other[k];
 }
 
+// Affine record (kAffWords words: x[12] y[12] inf): pk tables and the
+// verified-share table the combine reads.
+BD void store_aff(uint32_t* d, const G1A& p) {
+    store_fp(d, p.x);
+    store_fp(d + 12, p.y);
+    d[24] = p.inf ? 1u : 0u;
+}
+
 TDEC_KERNEL void tdec_pk_prepare(uint32_t n, const uint8_t* __restrict__ pk48,
                                                       uint32_t* __restrict__ pk_aff, int32_t* __restrict__ pk_status) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     G1A p;
     const bool ok = g1_decompress(pk48 + 48ull * k, p, true);
-    uint32_t* d = pk_aff + 32ull * k;
-    store_fp(d, p.x);
-    store_fp(d + 12, p.y);
-    d[24] = p.inf ? 1u : 0u;
+    store_aff(pk_aff + 32ull * k, p);
     pk_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
 }
 
@@ -766,7 +771,8 @@ TDEC_WAVE1_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restri
                                                          const uint32_t* __restrict__ coefW,
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const int32_t* __restrict__ pk_status,
-                                                         uint8_t* __restrict__ ok, const uint32_t* __restrict__ sel) {
+                                                         uint8_t* __restrict__ ok, const uint32_t* __restrict__ sel,
+                                                         uint32_t* __restrict__ share_aff) {
     const uint64_t i = grid_lane();
     if (i >= dev_count(n_dev, cap)) return;
     const uint64_t k = sel ? sel[i] : i;  // sel: share indices (batched path's failing leaves)
@@ -780,6 +786,7 @@ TDEC_WAVE1_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restri
     bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
     G1A s;
     if (good) good = g1_decompress(share48 + 48ull * k, s, true);
+    if (good && share_aff) store_aff(share_aff + (uint64_t)kAffWords * k, s);
     if (good) {
         const uint32_t* pa = pk_aff + 32ull * pk;
         const Fp pkx = load_fp(pa), pky = fp_neg(load_fp(pa + 12));
@@ -935,7 +942,8 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
                                                         const uint32_t* __restrict__ pk_aff,
                                                         const int32_t* __restrict__ pk_status,
                                                         const uint32_t* __restrict__ pk_tbl,
-                                                        uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
+                                                        uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok,
+                                                        uint32_t* __restrict__ share_aff) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (b >= dev_count(nb_dev, cap)) return;  // grid sized for the bound; the batch count is a device word
@@ -953,6 +961,7 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
     bool valid = in && ct_status[d.ct] == 0 && pk_status[pk] == 0;
     G1A s;
     if (valid) valid = g1_decompress(share48 + 48ull * k, s, true);
+    if (valid && share_aff) store_aff(share_aff + (uint64_t)kAffWords * k, s);  // for the combine
     // Weights are bound to the WHOLE batch (Fiat-Shamir): leaf digest
     // d_i = SHA3(U || S_i || pk_i), batch digest D = SHA3(d_0 || ... ),
     // r_i = SHA3(D || i)[0..8] | 1 — changing any share re-randomises every
@@ -1472,81 +1481,103 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
 }
 
 // PublicKeySet::decrypt as a bucket multi-scalar multiplication per G-lane
-// group (t + 1 <= G; G = 32: two ciphertexts per wave, G = 64: one), lane i
-// owning share i; same sum, same error precedence (DuplicateEntry before an
-// undecodable share) as the one-lane-per-ciphertext tdec_combine (kept for
-// t + 1 > 64):
-//  1. lane i < t + 1: DuplicateEntry / decode checks, lambda_i, its GLV halves
-//     (lambda_i = q x^2 + rm: [lambda_i]S_i = [rm]S_i + [q]([x^2]S_i), both
-//     < 2^129) — the 2(t + 1) affine points and their scalars go to LDS;
-//  2. every lane owns 2-bit windows of the 129-bit scalars (G = 32: windows
-//     2i, 2i + 1; G = 64: window i; the last lane also window 64): per window
+// group (G = 16: four ciphertexts per wave, t + 1 <= 24, lane i owning shares
+// i and i + 16; G = 32: two, t + 1 <= 32; G = 64: one, t + 1 <= 64); same
+// sum, same error precedence (DuplicateEntry before an undecodable share) as
+// the one-lane-per-ciphertext tdec_combine (kept for t + 1 > 64):
+//  1. per owned share: DuplicateEntry / decode checks (or, inside
+//     ThresholdDecrypt, the verification's decoded point: share_aff),
+//     lambda_i and its GLV halves (lambda_i = q x^2 + rm: [lambda_i]S_i =
+//     [rm]S_i + [q]([x^2]S_i), both < 2^129) — S_i (x, y, beta x) and the two
+//     scalars go to LDS;
+//  2. every lane owns kPer = 64 / G 2-bit windows of the 129-bit scalars (the
+//     last lane also window 64, whose digits are single bits): per window
 //     three buckets take one mixed addition per point whose digit is nonzero,
 //     W = b1 + 2 b2 + 3 b3, and the lane folds its windows by Horner;
 //  3. a log2(G)-level butterfly joins neighbouring lane ranges (the upper range
-//     shifted by its first window: 124 / 126 doublings on the critical path).
-// Per lane ~2,100 Fp multiplications for the sum at t = 21 against ~3,000 for
-// the per-lane joint double-and-add over the GLV halves it replaces (round 3,
-// profiles/r03z: 317 -> 231 ms per 100 k ciphertexts, TDec 4.65 -> 4.92 M
-// shares/s).
-template <int G>
+//     shifted by its first window: 2 kPer (G - 1) doublings on the critical path).
+// Fewer lanes per ciphertext cost more windows per lane but fewer butterfly
+// doublings per ciphertext: G = 16 issues ~30 % less per ciphertext than
+// G = 32 at t = 21 (round 4; round 3's G = 32 replaced a per-lane joint
+// double-and-add: 317 -> 231 ms per 100 k ciphertexts, profiles/r03z).
+template <int G, int MMAX>
 TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
                                   const uint32_t* __restrict__ idx, uint8_t* __restrict__ seeds,
-                                  int32_t* __restrict__ status) {
-    static_assert(G == 32 || G == 64, "group = half or whole wave");
-    constexpr uint32_t GPB = 64 / G;         // groups per 64-lane block
-    constexpr uint32_t kWin = 65;            // 2-bit windows of a 129-bit scalar
-    constexpr uint32_t kPer = 64 / G;        // windows per lane (the last lane: one more)
-    __shared__ uint32_t sPt[GPB][2 * G][24];  // affine S_i, [x^2]S_i
-    __shared__ uint32_t sSc[GPB][2 * G][5];   // rm_i, q_i (zero: no contribution)
-    const uint32_t gl = threadIdx.x / G, i = threadIdx.x & (G - 1), half = threadIdx.x & 32u & (uint32_t)(64 - G);
+                                  int32_t* __restrict__ status, const uint32_t* __restrict__ share_aff,
+                                  uint32_t n_nodes, const int32_t* __restrict__ pre_status) {
+    static_assert(G == 16 || G == 32 || G == 64, "a quarter, half or whole wave per ciphertext");
+    static_assert(MMAX <= 2 * G, "at most two shares per lane");
+    constexpr uint32_t GPB = 64 / G;                 // groups per 64-lane block
+    constexpr uint32_t kPer = 64 / G;                // 2-bit windows per lane (the last lane: one more)
+    constexpr uint32_t SPL = (MMAX + G - 1) / G;     // shares per lane
+    __shared__ uint32_t sPt[GPB][MMAX][36];          // S_i: x, y, beta x ([x^2]S_i = (beta x, -y))
+    __shared__ uint32_t sSc[GPB][2 * MMAX][5];       // point 2i: rm_i (S_i); 2i + 1: q_i ([x^2]S_i)
+    const uint32_t gl = threadIdx.x / G, i = threadIdx.x % G, gshift = gl * G;
     const uint32_t g = blockIdx.x * GPB + gl;
     const uint32_t m = t + 1;
     const bool live = g < n;  // no early return: the barrier and the group shuffles need every lane
-    const bool act = live && i < m;
     const uint32_t* ix = idx + (uint64_t)(live ? g : 0) * m;
-    const uint32_t me = act ? ix[i] : 0u;
-    bool dup = false;
-    if (act)
-        for (uint32_t j = i + 1; j < m; ++j) dup |= ix[j] == me;
-    G1A p = {fp_zero(), fp_zero(), true};
-    bool bad = false;
-    if (act) bad = !g1_decompress(share48 + ((uint64_t)g * m + i) * 48, p, false);
-    const uint64_t gmask = G == 64 ? ~0ull : 0xFFFFFFFFull;
-    const bool any_dup = (__ballot(dup) >> half) & gmask;
-    const bool any_bad = (__ballot(bad) >> half) & gmask;
-    const int32_t st = any_dup ? HBG_E_DUPLICATE_ENTRY : (any_bad ? HBG_E_INVALID_POINT : 0);
-    uint32_t q[5] = {0, 0, 0, 0, 0}, rm[5] = {0, 0, 0, 0, 0};
-    if (act && st == 0 && !p.inf) {
-        // lambda_i = prod_{j != i} x_j / prod_{j != i} (x_j - x_i),  x = index + 1  (mod r)
-        Fr num = fr_from_u32(1), den = fr_from_u32(1);
-        const Fr xi = fr_from_u32(me + 1);
-        for (uint32_t j = 0; j < m; ++j) {
-            if (j == i) continue;
-            const Fr xj = fr_from_u32(ix[j] + 1);
-            num = fr_mul(num, xj);
-            den = fr_mul(den, fr_sub(xj, xi));
+    // a failed selection (share_aff path): nothing to combine, the status is the selection's
+    const int32_t pre = (share_aff && pre_status && live) ? pre_status[g] : 0;
+    G1A p[SPL];
+    uint32_t me[SPL];
+    bool dup = false, bad = false;
+#pragma unroll
+    for (uint32_t r = 0; r < SPL; ++r) {
+        const uint32_t sI = i + G * r;
+        const bool act = live && sI < m;
+        me[r] = act ? ix[sI] : 0u;
+        p[r] = {fp_zero(), fp_zero(), true};
+        if (act)
+            for (uint32_t j = sI + 1; j < m; ++j) dup |= ix[j] == me[r];
+        if (act && pre == 0) {
+            if (share_aff) {  // the verification's decoded point (a selected share is a verified one)
+                const uint32_t* a =
+                    share_aff + ((uint64_t)g * n_nodes + (me[r] < n_nodes ? me[r] : 0u)) * kAffWords;
+                p[r].x = load_fp(a);
+                p[r].y = load_fp(a + 12);
+                p[r].inf = a[24] != 0;
+            } else {
+                bad |= !g1_decompress(share48 + ((uint64_t)g * m + sI) * 48, p[r], false);
+            }
         }
-        const Fr l = fr_canonical(fr_mul(num, fr_inv(den)));
-        uint32_t lw[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) lw[w] = l.v[w];
-        split_x2(lw, q, rm);
     }
-    // points 2i (S_i, scalar rm) and 2i + 1 ([x^2]S_i = (beta x, -y), scalar q);
-    // lanes past t + 1 write zero scalars for their slots
-    {
-        const Fp bx = fp_mul(p.x, fp_const(kBeta)), by = fp_neg(p.y);
-        uint32_t* a = sPt[gl][2 * i];
-        uint32_t* b = sPt[gl][2 * i + 1];
-        store_fp(a, p.x);
-        store_fp(a + 12, p.y);
-        store_fp(b, bx);
-        store_fp(b + 12, by);
+    const uint64_t gmask = G == 64 ? ~0ull : ((1ull << G) - 1ull);
+    const bool any_dup = (__ballot(dup) >> gshift) & gmask;
+    const bool any_bad = (__ballot(bad) >> gshift) & gmask;
+    const int32_t st = pre != 0 ? pre : (any_dup ? HBG_E_DUPLICATE_ENTRY : (any_bad ? HBG_E_INVALID_POINT : 0));
 #pragma unroll
-        for (int w = 0; w < 5; ++w) {
-            sSc[gl][2 * i][w] = rm[w];
-            sSc[gl][2 * i + 1][w] = q[w];
+    for (uint32_t r = 0; r < SPL; ++r) {
+        const uint32_t sI = i + G * r;
+        const bool act = live && sI < m;
+        uint32_t q[5] = {0, 0, 0, 0, 0}, rm[5] = {0, 0, 0, 0, 0};
+        if (act && st == 0 && !p[r].inf) {
+            // lambda_i = prod_{j != i} x_j / prod_{j != i} (x_j - x_i),  x = index + 1  (mod r)
+            Fr num = fr_from_u32(1), den = fr_from_u32(1);
+            const Fr xi = fr_from_u32(me[r] + 1);
+            for (uint32_t j = 0; j < m; ++j) {
+                if (j == sI) continue;
+                const Fr xj = fr_from_u32(ix[j] + 1);
+                num = fr_mul(num, xj);
+                den = fr_mul(den, fr_sub(xj, xi));
+            }
+            const Fr l = fr_canonical(fr_mul(num, fr_inv(den)));
+            uint32_t lw[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) lw[w] = l.v[w];
+            split_x2(lw, q, rm);
+        }
+        // shares past t + 1 keep zero scalars (no contribution)
+        if (sI < MMAX) {
+            uint32_t* a = sPt[gl][sI];
+            store_fp(a, p[r].x);
+            store_fp(a + 12, p[r].y);
+            store_fp(a + 24, fp_mul(p[r].x, fp_const(kBeta)));
+#pragma unroll
+            for (int w = 0; w < 5; ++w) {
+                sSc[gl][2 * sI][w] = rm[w];
+                sSc[gl][2 * sI + 1][w] = q[w];
+            }
         }
     }
     __syncthreads();
@@ -1562,8 +1593,12 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
         for (uint32_t j = 0; j < np; ++j) {
             const uint32_t d = (sSc[gl][j][word] >> sh) & 3u;
             if (!__any(d != 0)) continue;  // wave-uniform skip (no lane has this digit)
+            const uint32_t* pt = sPt[gl][j >> 1];
+            const Fp px = load_fp(pt + ((j & 1u) ? 24 : 0));
+            Fp py = load_fp(pt + 12);
+            if (j & 1u) py = fp_neg(py);
             const G1 sel = d == 1u ? b1 : (d == 2u ? b2 : b3);
-            const G1 sum = g1_add_mixed(sel, load_fp(sPt[gl][j]), load_fp(sPt[gl][j] + 12));
+            const G1 sum = g1_add_mixed(sel, px, py);
             if (d == 1u) b1 = sum;
             if (d == 2u) b2 = sum;
             if (d == 3u) b3 = sum;
@@ -1587,7 +1622,6 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
         for (uint32_t d = 0; d < dbls; ++d) x = g1_dbl(x);
         if (lower) L = g1_add(L, x);
     }
-    (void)kWin;
     if (!live || i != 0) return;
     status[g] = st;
     if (st != 0) return;
@@ -2247,12 +2281,13 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
                                      const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
                                      const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
                                      const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
-                                     const uint32_t* sel);
+                                     const uint32_t* sel, uint32_t* share_aff);
 hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t* ct_status, const uint32_t* coefH,
                                  const uint32_t* coefW, uint8_t* ok, hipStream_t st);
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
-                               uint32_t* scratch, uint8_t* seeds, hipStream_t st);
+                               uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff,
+                               uint32_t n_nodes, const int32_t* pre_status);
 hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
                            const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st);
 hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
@@ -2378,12 +2413,13 @@ hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const 
                                      const uint32_t* share_ct, const uint32_t* share_pk, const uint32_t* ct_u,
                                      const int32_t* ct_status, const uint32_t* coefH, const uint32_t* coefW,
                                      const uint32_t* pk_aff, const int32_t* pk_status, uint8_t* ok, hipStream_t st,
-                                     const uint32_t* sel) {
-    HBG_LAT_DISPATCH(cap, launch_tdec_verify_shares(cap, n_dev, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok, st, sel));
+                                     const uint32_t* sel, uint32_t* share_aff) {
+    HBG_LAT_DISPATCH(cap, launch_tdec_verify_shares(cap, n_dev, share48, share_ct, share_pk, ct_u, ct_status, coefH, coefW, pk_aff, pk_status, ok, st, sel, share_aff));
     HBG_COUNT_MARK("tdec_verify_shares", st);
     if (cap == 0) return hipSuccess;
     tdec_verify_shares<<<item_grid(cap), dim3(64), 0, st>>>(cap, n_dev, share48, share_ct, share_pk, ct_u,
-                                                                ct_status, coefH, coefW, pk_aff, pk_status, ok, sel);
+                                                                ct_status, coefH, coefW, pk_aff, pk_status, ok, sel,
+                                                                share_aff);
     return hipGetLastError();
 }
 
@@ -2453,11 +2489,11 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
                                     const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
-                                    uint8_t* leaf_ok, hipStream_t st) {
+                                    uint8_t* leaf_ok, hipStream_t st, uint32_t* share_aff) {
     HBG_COUNT_MARK("tdec_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
     tdec_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_max, nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
-                                                         pk_aff, pk_status, pk_tbl, sums, leaf_ok);
+                                                         pk_aff, pk_status, pk_tbl, sums, leaf_ok, share_aff);
     return hipGetLastError();
 }
 
@@ -2513,15 +2549,23 @@ hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t
 }
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
-                               uint32_t* scratch, uint8_t* seeds, hipStream_t st) {
-    HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 32 ? 32u : 64u), launch_tdec_combine(n, t, share48, idx, V, V_off, out, status, scratch, seeds, st));
+                               uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff,
+                               uint32_t n_nodes, const int32_t* pre_status) {
+    HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 24 ? 16u : (t + 1 <= 32 ? 32u : 64u)),
+                     launch_tdec_combine(n, t, share48, idx, V, V_off, out, status, scratch, seeds, st, share_aff,
+                                         n_nodes, pre_status));
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     HBG_GRID_CHECK(n, 64);  // every grid of this call, before the first launch
-    if (t + 1 <= 32)
-        tdec_combine_msm<32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
+    if (t + 1 <= 24)
+        tdec_combine_msm<16, 24><<<dim3((n + 3) / 4), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status,
+                                                                         share_aff, n_nodes, pre_status);
+    else if (t + 1 <= 32)
+        tdec_combine_msm<32, 32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status,
+                                                                         share_aff, n_nodes, pre_status);
     else if (t + 1 <= 64)
-        tdec_combine_msm<64><<<dim3(n), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status);
+        tdec_combine_msm<64, 64><<<dim3(n), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, share_aff,
+                                                               n_nodes, pre_status);
     else
         tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, scratch);
     hipError_t e = hipGetLastError();
