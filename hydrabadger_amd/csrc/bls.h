@@ -22,7 +22,11 @@
 #include <stdint.h>
 
 #include "bls_consts.h"
+#ifdef HBG_FP_SUB_HEADER  // tool builds only (tools/build_variant.py): another generated body
+#include HBG_FP_SUB_HEADER
+#else
 #include "bls_fp_sub.h"
+#endif
 
 namespace hbg {
 namespace bls {

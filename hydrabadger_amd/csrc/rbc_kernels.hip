@@ -715,9 +715,38 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     u32x2_a4 pre[D];  // the next interior pass's payload windows, loaded during this pass's Keccak work
     r.pre = pre;
     bool have_pre = false;
+    // A data lane's absorb block comes from the payload (payload_block) unless
+    // it touches the length prefix or the padding (then the shard row just
+    // stored).  The first block a sweep absorbs is loaded at the top of the
+    // pass, BEFORE the pass's 64 row stores: vmcnt is one in-order counter, so
+    // a load issued after them waits for their (nt, HBM) acknowledgements.
+    auto payload_block = [&](uint32_t blk) {
+        return (uint64_t)t * L + 136ull * blk >= 4 && (uint64_t)t * L + 136ull * blk + 140 <= P + 4;
+    };
+    uint32_t pd[35];  // the raw payload dwords of that block (aligned view)
+    auto fetch_payload_block = [&](uint32_t blk) {
+        const uint64_t o = (uint64_t)t * L + 136ull * blk - 4;
+        const uint32_t a0 = (uint32_t)(o & ~3ull);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r.py, (uint32_t)(sub * pstride) + a0 + 8 * i, 0, 0);
+            pd[2 * i] = v[0];
+            pd[2 * i + 1] = v[1];
+        }
+        pd[34] = __builtin_amdgcn_raw_buffer_load_b32(r.py, (uint32_t)(sub * pstride) + a0 + 136, 0, 0);
+    };
+    // the first block at which the last data row (the first to leave the
+    // payload) reads its shard row: 136 b > P + 4 - 140 - (D - 1) L
+    const uint64_t tail_blk = (P + 4 >= (uint64_t)(D - 1) * L + 140)
+                                  ? (P + 4 - (uint64_t)(D - 1) * L - 140) / 136 + 1
+                                  : 0;
     for (uint32_t ps = 0; ps < passes; ++ps) {
         const uint32_t p0 = ps * LPI, p = p0 + t;  // this lane's column in the encode pass
         r.p0 = p0;
+        const uint64_t avail_now = 4ull * LPI * (ps + 1) < L ? 4ull * LPI * (ps + 1) : L;
+        const bool first_due = (uint64_t)(done + 1) * 136 <= avail_now;  // wave-uniform
+        const bool have_pd = first_due && row_lane && !ring_lane && payload_block(done);
+        if (have_pd) fetch_payload_block(done);
         // ring position of this lane's column (wave-uniform pass start; a pass may wrap)
         uint32_t wpos = (uint32_t)(((uint64_t)ps * 4 * LPI) % R) + 4 * t;
         if (wpos >= R) wpos -= R;
@@ -731,12 +760,14 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                 encode_word<D, Q, 1, true>(r);
             }
         }
-        // the pass's stores are complete in L2 (data rows) and in LDS (parity
-        // rows) before any lane reads them back
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
         const uint64_t written = 4ull * LPI * (ps + 1);
         const uint64_t avail = written < L ? written : L;
+        // a sweep whose blocks include one read back from a shard row (block 0:
+        // the length prefix; from tail_blk on: the padding) first waits for the
+        // pass's stores; LDS (parity rows) is ordered by the barrier
+        const uint32_t last_blk = (uint32_t)(avail / 136);  // exclusive
+        if (done == 0 || last_blk > tail_blk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         const bool next_pre = live && ps + 1 < passes && interior(ps + 1);
         have_pre = false;
         auto prefetch = [&]() {
@@ -747,16 +778,26 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             }
             have_pre = next_pre;
         };
+        bool first = true;
         while ((uint64_t)(done + 1) * 136 <= avail) {
             if (row_lane) {
                 uint64_t w[17];
-                load_block(w);
+                if (first && have_pd) {
+                    const uint32_t sh8 = (uint32_t)(((uint64_t)t * L + 136ull * done - 4) & 3);
+#pragma unroll
+                    for (int i = 0; i < 17; ++i)
+                        w[i] = (uint64_t)__builtin_amdgcn_alignbyte(pd[2 * i + 1], pd[2 * i], sh8) |
+                               ((uint64_t)__builtin_amdgcn_alignbyte(pd[2 * i + 2], pd[2 * i + 1], sh8) << 32);
+                } else {
+                    load_block(w);
+                }
 #pragma unroll
                 for (int i = 0; i < 17; ++i) {
                     a[i].lo ^= (uint32_t)w[i];
                     a[i].hi ^= (uint32_t)(w[i] >> 32);
                 }
             }
+            first = false;
             // next pass's payload loads: behind this block's loads (vmcnt is
             // in order), ahead of a whole permutation
             prefetch();
@@ -768,6 +809,7 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         __syncthreads();
     }
     uint32_t d[8];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the final block may read a stored shard row
     if (row_lane) {
         // final (possibly empty) block: bytes [136 done, L) + FIPS-202 padding.
         // Reads stay below round_up(L, 8) <= S (rows) / inside the ring.

@@ -47,6 +47,7 @@ S_MASK = 84     # s[84:85]
 S_TGT = 86      # s[86:87] call target
 S_CARRY2 = 88   # s[88+2k : 89+2k]: the second carry set (partial products alternate sets)
 VALU_SGPR_WAIT = 2  # wait states between a VALU SGPR write and a VALU read of it
+PIPELINE = True     # --no-pipeline: count each product's carries right after its mads (round 3's order)
 
 
 class Emitter:
@@ -135,7 +136,7 @@ def gen_sub(N: int) -> str:
 
         pending = None
         for q, (xk, xi, yk, yi) in enumerate(prods):
-            cs = q % 2
+            cs = q % 2 if PIPELINE else 0
             for s in slots:
                 def op(kind, i):
                     if kind == "p":
@@ -147,6 +148,9 @@ def gen_sub(N: int) -> str:
             if pending is not None:
                 counts(pending)
             pending = cs
+            if not PIPELINE:
+                counts(cs)
+                pending = None
         if pending is not None:
             counts(pending)
 
@@ -202,8 +206,12 @@ def gen_sub(N: int) -> str:
 def clobbers(N: int, nv: int) -> str:
     # VGPRs the subroutine writes besides the outputs X_k: all temporaries
     vs = [f'"v{i}"' for i in range(24 * N, nv)]
-    ss = [f'"s{i}"' for i in range(S_P, S_CARRY2 + 6)] + ['"s30"', '"s31"', '"scc"']
+    top = S_CARRY2 + 6 if PIPELINE else S_TGT + 2
+    ss = [f'"s{i}"' for i in range(S_P, top)] + ['"s30"', '"s31"', '"scc"']
     return ", ".join(vs + ss)
+
+
+OUT = None
 
 
 def main():
@@ -237,11 +245,17 @@ def main():
         f"#define HBG_FP_SUB3_CLOBBERS {cl[3]}\n\n",
         "}  // namespace bls\n}  // namespace hbg\n",
     ]
-    path = os.path.join(ROOT, "hydrabadger_amd", "csrc", "bls_fp_sub.h")
+    path = OUT or os.path.join(ROOT, "hydrabadger_amd", "csrc", "bls_fp_sub.h")
     with open(path, "w") as f:
         f.write("".join(out))
     print(path)
 
 
 if __name__ == "__main__":
+    import sys
+    OUT = None
+    if "--no-pipeline" in sys.argv:
+        PIPELINE = False
+    if "--out" in sys.argv:
+        OUT = sys.argv[sys.argv.index("--out") + 1]
     main()
