@@ -778,11 +778,11 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             }
             have_pre = next_pre;
         };
-        bool first = true;
+        bool use_pd = have_pd;  // pd holds this block's payload dwords (this lane)
         while ((uint64_t)(done + 1) * 136 <= avail) {
             if (row_lane) {
                 uint64_t w[17];
-                if (first && have_pd) {
+                if (use_pd) {
                     const uint32_t sh8 = (uint32_t)(((uint64_t)t * L + 136ull * done - 4) & 3);
 #pragma unroll
                     for (int i = 0; i < 17; ++i)
@@ -797,7 +797,14 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
                     a[i].hi ^= (uint32_t)(w[i] >> 32);
                 }
             }
-            first = false;
+            // the sweep's next block (a data lane, from the payload): loaded
+            // before this block's permutation, its latency hidden under it
+#ifndef HBG_ENC_NO_SWEEP_PD  // A/B switch: the sweep's later blocks from load_block
+            use_pd = (uint64_t)(done + 2) * 136 <= avail && row_lane && !ring_lane && payload_block(done + 1);
+            if (use_pd) fetch_payload_block(done + 1);
+#else
+            use_pd = false;
+#endif
             // next pass's payload loads: behind this block's loads (vmcnt is
             // in order), ahead of a whole permutation
             prefetch();
@@ -984,6 +991,18 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         uint32_t wpos = (uint32_t)(((uint64_t)ps * 256) % R) + 4 * t;
         if (wpos >= R) wpos -= R;
         uint32_t* rcol = ring + wpos / 4;
+        // a present row's first block of this pass's sweep is loaded here,
+        // BEFORE the pass's stores (vmcnt is one in-order counter: a load
+        // issued after them waits for their acknowledgements); missing rows
+        // come from the ring after the barrier
+        const uint64_t avail_now = 256ull * (ps + 1) < L ? 256ull * (ps + 1) : L;
+        uint64_t w[17];
+#ifndef HBG_DEC_NO_PRESTORE  // A/B switch: the first block loaded after the barrier
+        bool have_w = !row_missing && (uint64_t)(done + 1) * 136 <= avail_now;
+#else
+        bool have_w = false && avail_now;
+#endif
+        if (have_w) load_block(w, 17, done);
         for (uint64_t m = warm; m; m &= m - 1ull) {  // uniform loop, per-lane guard inside
             const uint32_t r = (uint32_t)__builtin_ctzll(m);
             const uint32_t so = __builtin_amdgcn_readfirstlane(r * (uint32_t)S + 4 * p0);
@@ -1113,8 +1132,6 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         };
         // the next block of the same sweep is loaded before this block's
         // permutation (its latency hides under it)
-        uint64_t w[17];
-        bool have_w = false;
         while ((uint64_t)(done + 1) * 136 <= avail) {
             if (!have_w) load_block(w, 17, done);
 #pragma unroll

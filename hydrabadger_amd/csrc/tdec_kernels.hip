@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "bls.h"
@@ -296,9 +297,9 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-__global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8_t* __restrict__ V,
-                                                         const uint64_t* __restrict__ off,
-                                                         uint8_t* __restrict__ dig) {
+__global__ __launch_bounds__(64) void tdec_v_digest_wave64(uint64_t n, const uint8_t* __restrict__ V,
+                                                           const uint64_t* __restrict__ off,
+                                                           uint8_t* __restrict__ dig) {
     const uint64_t k = blockIdx.x;
     if (k >= n) return;
     const uint64_t o = off[k], len = off[k + 1] - o;
@@ -387,6 +388,171 @@ __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8
             d[b] = (uint8_t)(lo >> (8 * b));
             d[4 + b] = (uint8_t)(hi >> (8 * b));
         }
+    }
+}
+
+// Round 4: the same wave sponge on BIT-INTERLEAVED 32-bit halves, one half
+// per lane (lane 2i + h holds the even (h = 0) or odd (h = 1) bits of state
+// word i, the standard 32-bit Keccak representation).  A 64-bit rotation by
+// r is then a 32-bit rotation of one half — by r/2 when r is even, and by
+// (r±1)/2 of the OTHER half when r is odd — so every cross-lane move is one
+// ds_bpermute of one dword instead of two: per round 4 (column parity) + 2
+// (C[x-1], rotl(C[x+1], 1)) + 3 (pi sources of chi) gathers in three
+// dependent stages and 7 VALU, against 18 gathers and ~35 VALU for the
+// (lo, hi)-per-lane sponge above.  The odd-r half swap is folded into the
+// gather addresses: a source lane pre-rotates its half by the amount its one
+// pi destination needs, and a destination of half h reads half h ^ (r & 1).
+// Message words are de-interleaved on absorption (prepared for the next block
+// in the middle of the current permutation) and re-interleaved for the
+// digest.
+constexpr uint64_t kKeccakRC64[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+constexpr uint32_t even_bits64(uint64_t w) {
+    uint32_t r = 0;
+    for (int i = 0; i < 32; ++i) r |= (uint32_t)((w >> (2 * i)) & 1u) << i;
+    return r;
+}
+__device__ __forceinline__ uint32_t compress_even32(uint32_t x) {  // bits 0, 2, .., 30 -> 0 .. 15
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    return (x | (x >> 8)) & 0x0000FFFFu;
+}
+__device__ __forceinline__ uint32_t spread_even16(uint32_t x) {  // bits 0 .. 15 -> 0, 2, .., 30
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
+__device__ __forceinline__ uint32_t bperm(uint32_t addr, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)v);
+}
+
+__global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8_t* __restrict__ V,
+                                                         const uint64_t* __restrict__ off,
+                                                         uint8_t* __restrict__ dig) {
+    const uint64_t k = blockIdx.x;
+    if (k >= n) return;
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    if (len <= 64) return;  // hashed inline by hash_g1_g2_msg's caller
+    // lanes 50..63 shadow lanes 0..13 (never read, never absorb or store)
+    const uint32_t l = threadIdx.x, ls = l < 50 ? l : l - 50;
+    const uint32_t i = ls >> 1, h = ls & 1u, x = i % 5, y = i / 5;
+    auto addr = [](uint32_t word, uint32_t half) { return (2 * word + half) << 2; };
+    uint32_t acol[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acol[j] = addr(x + 5 * ((y + 1 + j) % 5), h);
+    // D[x] = C[x-1] ^ rotl64(C[x+1], 1): even half = C[x-1].e ^ rotl32(C[x+1].o, 1), odd = C[x-1].o ^ C[x+1].e
+    const uint32_t acm = addr((x + 4) % 5 + 5 * y, h), acp = addr((x + 1) % 5 + 5 * y, h ^ 1u);
+    const uint32_t scp = h ? 0u : 31u;
+    const uint32_t r = kRhoOff[i];
+    const uint32_t amt = (r & 1u) ? (h ? (r + 1) / 2 : (r - 1) / 2) : r / 2;
+    const uint32_t srho = (32u - amt) & 31u;  // alignbit(v, v, s) = rotr32(v, s)
+    auto pisrc = [](uint32_t X, uint32_t Y) { return (3 * (Y + 15 - 3 * X)) % 5 + 5 * X; };
+    auto srcaddr = [&](uint32_t X, uint32_t Y) {
+        const uint32_t s = pisrc(X, Y);
+        return addr(s, h ^ (kRhoOff[s] & 1u));
+    };
+    const uint32_t ab0 = srcaddr(x, y), ab1 = srcaddr((x + 1) % 5, y), ab2 = srcaddr((x + 2) % 5, y);
+    const uint32_t m_e = l == 0 ? 0xFFFFFFFFu : 0u, m_o = l == 1 ? 0xFFFFFFFFu : 0u;
+    const bool msg_lane = l < 34;
+    const uint32_t li = msg_lane ? i : 0u;
+    const uint8_t* p = V + o;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+    const uint64_t nfull = len / 136;
+    uint32_t d0 = 0, d1 = 0, d2 = 0, nxt = 0;
+    auto fetch = [&](uint64_t b) {
+        const uint32_t* qb = q + 34 * b + 2 * li;
+        d0 = qb[0];
+        d1 = qb[1];
+        d2 = sh ? qb[2] : 0u;
+    };
+    // this lane's interleaved half of the 64-bit message word (wl, wh)
+    auto half_of = [&](uint32_t wl, uint32_t wh) {
+        const uint32_t v = compress_even32(wl >> h) | (compress_even32(wh >> h) << 16);
+        return msg_lane ? v : 0u;
+    };
+    auto prepare = [&]() {
+        nxt = half_of(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh));
+    };
+    uint32_t s = 0;
+    auto permute = [&](bool hook) {
+#pragma unroll
+        for (int rnd = 0; rnd < 24; ++rnd) {
+            const uint32_t g0 = bperm(acol[0], s), g1 = bperm(acol[1], s);
+            const uint32_t g2 = bperm(acol[2], s), g3 = bperm(acol[3], s);
+            const uint32_t c = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(s, g0, g1, 0x96), g2, g3, 0x96);
+            const uint32_t cm = bperm(acm, c), cp = bperm(acp, c);
+            s = __builtin_amdgcn_bitop3_b32(s, cm, __builtin_amdgcn_alignbit(cp, cp, scp), 0x96);
+            const uint32_t rv = __builtin_amdgcn_alignbit(s, s, srho);
+            const uint32_t b0 = bperm(ab0, rv), b1 = bperm(ab1, rv), b2 = bperm(ab2, rv);
+            constexpr uint32_t kE[24] = {
+                even_bits64(kKeccakRC64[0]), even_bits64(kKeccakRC64[1]), even_bits64(kKeccakRC64[2]),
+                even_bits64(kKeccakRC64[3]), even_bits64(kKeccakRC64[4]), even_bits64(kKeccakRC64[5]),
+                even_bits64(kKeccakRC64[6]), even_bits64(kKeccakRC64[7]), even_bits64(kKeccakRC64[8]),
+                even_bits64(kKeccakRC64[9]), even_bits64(kKeccakRC64[10]), even_bits64(kKeccakRC64[11]),
+                even_bits64(kKeccakRC64[12]), even_bits64(kKeccakRC64[13]), even_bits64(kKeccakRC64[14]),
+                even_bits64(kKeccakRC64[15]), even_bits64(kKeccakRC64[16]), even_bits64(kKeccakRC64[17]),
+                even_bits64(kKeccakRC64[18]), even_bits64(kKeccakRC64[19]), even_bits64(kKeccakRC64[20]),
+                even_bits64(kKeccakRC64[21]), even_bits64(kKeccakRC64[22]), even_bits64(kKeccakRC64[23])};
+            constexpr uint32_t kO[24] = {
+                even_bits64(kKeccakRC64[0] >> 1), even_bits64(kKeccakRC64[1] >> 1), even_bits64(kKeccakRC64[2] >> 1),
+                even_bits64(kKeccakRC64[3] >> 1), even_bits64(kKeccakRC64[4] >> 1), even_bits64(kKeccakRC64[5] >> 1),
+                even_bits64(kKeccakRC64[6] >> 1), even_bits64(kKeccakRC64[7] >> 1), even_bits64(kKeccakRC64[8] >> 1),
+                even_bits64(kKeccakRC64[9] >> 1), even_bits64(kKeccakRC64[10] >> 1),
+                even_bits64(kKeccakRC64[11] >> 1), even_bits64(kKeccakRC64[12] >> 1),
+                even_bits64(kKeccakRC64[13] >> 1), even_bits64(kKeccakRC64[14] >> 1),
+                even_bits64(kKeccakRC64[15] >> 1), even_bits64(kKeccakRC64[16] >> 1),
+                even_bits64(kKeccakRC64[17] >> 1), even_bits64(kKeccakRC64[18] >> 1),
+                even_bits64(kKeccakRC64[19] >> 1), even_bits64(kKeccakRC64[20] >> 1),
+                even_bits64(kKeccakRC64[21] >> 1), even_bits64(kKeccakRC64[22] >> 1),
+                even_bits64(kKeccakRC64[23] >> 1)};
+            s = __builtin_amdgcn_bitop3_b32(b0, b1, b2, 0xd2) ^ (m_e & kE[rnd]) ^ (m_o & kO[rnd]);
+            if (hook && rnd == 11) prepare();  // the next block's dwords have long arrived
+        }
+    };
+    if (nfull) {
+        fetch(0);
+        prepare();
+    }
+    for (uint64_t b = 0; b < nfull; ++b) {
+        s ^= nxt;
+        const bool more = b + 1 < nfull;
+        if (more) fetch(b + 1);  // in flight during this permutation
+        permute(more);
+    }
+    // final block: bytes [136 nfull, len) + FIPS-202 padding 0x06 .. 0x80
+    const uint32_t rem = (uint32_t)(len - 136 * nfull);
+    uint32_t wl = 0, wh = 0;
+    if (msg_lane) {
+        for (uint32_t t = 0; t < 8; ++t) {
+            const uint32_t pos = 8 * li + t;
+            uint32_t byte = pos < rem ? (uint32_t)p[136 * nfull + pos] : 0u;
+            if (pos == rem) byte ^= 0x06u;
+            if (pos == 135) byte ^= 0x80u;
+            if (t < 4) wl |= byte << (8 * t);
+            else wh |= byte << (8 * (t - 4));
+        }
+    }
+    s ^= half_of(wl, wh);
+    permute(false);
+    // digest: words 0..3 = lanes 0..7; lane 2w + h writes bytes 8w + 4h .. + 3
+    const uint32_t partner = bperm((l ^ 1u) << 2, s);
+    const uint32_t e = h ? partner : s, od = h ? s : partner;
+    const uint32_t es = h ? e >> 16 : e, os = h ? od >> 16 : od;
+    const uint32_t w32 = spread_even16(es) | (spread_even16(os) << 1);
+    if (l < 8) {
+        uint8_t* d = dig + 32 * k + 4 * l;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) d[b] = (uint8_t)(w32 >> (8 * b));
     }
 }
 
@@ -2354,7 +2520,13 @@ hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_
     HBG_COUNT_MARK("tdec_v_digest", st);
     if (n == 0) return hipSuccess;
     HBG_GRID_CHECK((n + 63) / 64, 64);
-    if (n <= kVDigestWaveMax)  // few items (the epoch's contributions): one wave per sponge
+    static const bool wave64 = std::getenv("HBG_SHA3_WAVE64") != nullptr;  // A/B: the (lo, hi)-per-lane sponge
+    static const uint64_t wave_max = std::getenv("HBG_VDIGEST_WAVE_MAX")  // A/B of the cut
+                                         ? std::strtoull(std::getenv("HBG_VDIGEST_WAVE_MAX"), nullptr, 10)
+                                         : kVDigestWaveMax;
+    if (n <= wave_max && wave64)
+        tdec_v_digest_wave64<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
+    else if (n <= wave_max)  // few items (the epoch's contributions): one wave per sponge
         tdec_v_digest_wave<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
     else
         tdec_v_digest<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(n, V, V_off, dig);
