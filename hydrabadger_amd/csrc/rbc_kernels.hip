@@ -799,12 +799,9 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
             }
             // the sweep's next block (a data lane, from the payload): loaded
             // before this block's permutation, its latency hidden under it
-#ifndef HBG_ENC_NO_SWEEP_PD  // A/B switch: the sweep's later blocks from load_block
-            use_pd = (uint64_t)(done + 2) * 136 <= avail && row_lane && !ring_lane && payload_block(done + 1);
-            if (use_pd) fetch_payload_block(done + 1);
-#else
+            // (an in-sweep prefetch of the next payload block into pd measured
+            // 1.3 % slower: 26.71 against 26.37 ms, gpurun_out r04u)
             use_pd = false;
-#endif
             // next pass's payload loads: behind this block's loads (vmcnt is
             // in order), ahead of a whole permutation
             prefetch();
@@ -991,17 +988,11 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         uint32_t wpos = (uint32_t)(((uint64_t)ps * 256) % R) + 4 * t;
         if (wpos >= R) wpos -= R;
         uint32_t* rcol = ring + wpos / 4;
-        // a present row's first block of this pass's sweep is loaded here,
-        // BEFORE the pass's stores (vmcnt is one in-order counter: a load
-        // issued after them waits for their acknowledgements); missing rows
-        // come from the ring after the barrier
-        const uint64_t avail_now = 256ull * (ps + 1) < L ? 256ull * (ps + 1) : L;
+        // the sweep's first block is loaded after the barrier (loading a
+        // present row's block here, before the pass's stores, measured 1.8 %
+        // slower: 39.2 against 38.6 ms, gpurun_out r04u)
         uint64_t w[17];
-#ifndef HBG_DEC_NO_PRESTORE  // A/B switch: the first block loaded after the barrier
-        bool have_w = !row_missing && (uint64_t)(done + 1) * 136 <= avail_now;
-#else
-        bool have_w = false && avail_now;
-#endif
+        bool have_w = false;
         if (have_w) load_block(w, 17, done);
         for (uint64_t m = warm; m; m &= m - 1ull) {  // uniform loop, per-lane guard inside
             const uint32_t r = (uint32_t)__builtin_ctzll(m);

@@ -435,6 +435,7 @@ __device__ __forceinline__ uint32_t bperm(uint32_t addr, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)v);
 }
 
+template <bool kTwoStage>
 __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8_t* __restrict__ V,
                                                          const uint64_t* __restrict__ off,
                                                          uint8_t* __restrict__ dig) {
@@ -451,6 +452,14 @@ __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8
     for (int j = 0; j < 4; ++j) acol[j] = addr(x + 5 * ((y + 1 + j) % 5), h);
     // D[x] = C[x-1] ^ rotl64(C[x+1], 1): even half = C[x-1].e ^ rotl32(C[x+1].o, 1), odd = C[x-1].o ^ C[x+1].e
     const uint32_t acm = addr((x + 4) % 5 + 5 * y, h), acp = addr((x + 1) % 5 + 5 * y, h ^ 1u);
+    // kTwoStage: D from the 5 + 5 words of columns x-1 and x+1 in ONE gather
+    // stage (C[x] itself is never needed): 13 gathers in two dependent stages
+    uint32_t am5[5], ap5[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        am5[j] = addr((x + 4) % 5 + 5 * j, h);
+        ap5[j] = addr((x + 1) % 5 + 5 * j, h ^ 1u);
+    }
     const uint32_t scp = h ? 0u : 31u;
     const uint32_t r = kRhoOff[i];
     const uint32_t amt = (r & 1u) ? (h ? (r + 1) / 2 : (r - 1) / 2) : r / 2;
@@ -487,11 +496,25 @@ __global__ __launch_bounds__(64) void tdec_v_digest_wave(uint64_t n, const uint8
     auto permute = [&](bool hook) {
 #pragma unroll
         for (int rnd = 0; rnd < 24; ++rnd) {
-            const uint32_t g0 = bperm(acol[0], s), g1 = bperm(acol[1], s);
-            const uint32_t g2 = bperm(acol[2], s), g3 = bperm(acol[3], s);
-            const uint32_t c = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(s, g0, g1, 0x96), g2, g3, 0x96);
-            const uint32_t cm = bperm(acm, c), cp = bperm(acp, c);
-            s = __builtin_amdgcn_bitop3_b32(s, cm, __builtin_amdgcn_alignbit(cp, cp, scp), 0x96);
+            if constexpr (kTwoStage) {
+                uint32_t m[5], q5[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) m[j] = bperm(am5[j], s);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) q5[j] = bperm(ap5[j], s);
+                const uint32_t cm = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(m[0], m[1], m[2], 0x96),
+                                                                m[3], m[4], 0x96);
+                const uint32_t cp = __builtin_amdgcn_bitop3_b32(
+                    __builtin_amdgcn_bitop3_b32(q5[0], q5[1], q5[2], 0x96), q5[3], q5[4], 0x96);
+                s = __builtin_amdgcn_bitop3_b32(s, cm, __builtin_amdgcn_alignbit(cp, cp, scp), 0x96);
+            } else {
+                const uint32_t g0 = bperm(acol[0], s), g1 = bperm(acol[1], s);
+                const uint32_t g2 = bperm(acol[2], s), g3 = bperm(acol[3], s);
+                const uint32_t c =
+                    __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(s, g0, g1, 0x96), g2, g3, 0x96);
+                const uint32_t cm = bperm(acm, c), cp = bperm(acp, c);
+                s = __builtin_amdgcn_bitop3_b32(s, cm, __builtin_amdgcn_alignbit(cp, cp, scp), 0x96);
+            }
             const uint32_t rv = __builtin_amdgcn_alignbit(s, s, srho);
             const uint32_t b0 = bperm(ab0, rv), b1 = bperm(ab1, rv), b2 = bperm(ab2, rv);
             constexpr uint32_t kE[24] = {
@@ -2521,13 +2544,16 @@ hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_
     if (n == 0) return hipSuccess;
     HBG_GRID_CHECK((n + 63) / 64, 64);
     static const bool wave64 = std::getenv("HBG_SHA3_WAVE64") != nullptr;  // A/B: the (lo, hi)-per-lane sponge
+    static const bool three_stage = std::getenv("HBG_SHA3_3STAGE") != nullptr;  // A/B: theta in two stages
     static const uint64_t wave_max = std::getenv("HBG_VDIGEST_WAVE_MAX")  // A/B of the cut
                                          ? std::strtoull(std::getenv("HBG_VDIGEST_WAVE_MAX"), nullptr, 10)
                                          : kVDigestWaveMax;
     if (n <= wave_max && wave64)
         tdec_v_digest_wave64<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
+    else if (n <= wave_max && three_stage)
+        tdec_v_digest_wave<false><<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
     else if (n <= wave_max)  // few items (the epoch's contributions): one wave per sponge
-        tdec_v_digest_wave<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
+        tdec_v_digest_wave<true><<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
     else
         tdec_v_digest<<<dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, st>>>(n, V, V_off, dig);
     return hipGetLastError();
