@@ -403,6 +403,9 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             "verify_only": {"achieved": achieved_v / 1e12, "frac": achieved_v / MAD_PEAK,
                             "fp_mul_per_share": per_share_v},
             "traffic": None, "count_source": prof["path"] + " (" + prof.get("source", "") + ")",
+            "count_note": "the combine's count predates its reuse of the verified shares' affine points (no second "
+                          "decompression): ~140 of its 818 Fp ops per share are no longer executed, so the whole-"
+                          "call count is ~2 % high; the instrumented build of HEAD faults (DESIGN.md §5)",
             "peak_source": "v_mad_u64_u32 4.44 cyc/wave-instr/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) "
                            "x 1024 SIMDs x 64 lanes x 2.4 GHz",
             "note": "each Fp mul also issues 288 v_addc (carry) + ~95 other VALU: frac <= ~0.5 by construction",
