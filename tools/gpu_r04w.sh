@@ -22,7 +22,7 @@ ps -u "$(id -u)" -o pid,ppid,etime,cmd > "$OUT/ps_after.txt" 2>&1
 python3 - "$OUT/bench.json" <<'EOF'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print("headline", round(d["value"] / 1e9, 1), "GB/s", round(d["ms_per_step"], 2), "ms", "frac", round(d["roofline"]["frac"], 3))
+print("headline", round(d["value"], 1), d["unit"], round(d["ms_per_step"], 2), "ms", "frac", round(d["roofline"]["frac"], 3))
 for k in ("decode", "tdec", "network_epoch", "config1_n16"):
     v = d.get(k)
     if isinstance(v, dict):
