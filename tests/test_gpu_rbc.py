@@ -558,3 +558,40 @@ def test_fused_decode_matches_three_launch_decode(P, n):
         assert (ref is None) == (s1[k] == 0), k
         if ref is not None:
             assert o1[k, :len(ref)].tobytes() == ref, k
+
+
+def test_fused_decode_many_erasure_patterns():
+    """The fused decoder over 1,024 instances with independent random 2f
+    erasures (every count of missing data rows the distribution reaches, so
+    every group of the run-time coder runs with padding rows in it): each
+    payload comes back and every rebuilt shard row equals the encoder's."""
+    torch = _torch()
+    bc = _bc()
+    from hydrabadger_amd import _lib
+    N, P, n = 64, 16384 + 5, 1024
+    pay, shards, levels, L, S = _device_batch(N, P, n, first=3000)
+    data, parity = bc.shard_counts(N)
+    nodes = levels.shape[1]
+    pm = np.stack([synth.erasure_mask(3000 + k, N, parity) for k in range(n)]).astype(np.uint8)
+    missing_data = (pm[:, :data] == 0).sum(1)
+    assert missing_data.min() <= 10 and missing_data.max() >= 19
+    present = torch.from_numpy(pm).to("cuda:0")
+    roots = levels[:, nodes - 1, :].contiguous()
+    OS = (data * L + 15) // 16 * 16
+    ctx = _lib.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        _lib.check(_lib.lib().hbg_test_set_rbc_decode_fused(ctx.h, 1))
+        dmg = shards.clone()
+        dmg[present == 0] = 0x5A
+        out = torch.zeros((n, OS), dtype=torch.uint8, device="cuda:0")
+        plen = torch.zeros(n, dtype=torch.int64, device="cuda:0")
+        st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+        bc.rbc_decode_batch(N, L, dmg, present, roots, out, plen, st, ctx=ctx, device=True)
+        torch.cuda.synchronize()
+    finally:
+        ctx.close()
+    assert st.cpu().tolist() == [1] * n
+    assert plen.cpu().tolist() == [P] * n
+    assert torch.equal(out[:, :P], pay[:, :P])
+    assert torch.equal(dmg[:, :, :L], shards[:, :, :L])
