@@ -258,8 +258,8 @@ def tdec_pmc_traffic(n_shares: int) -> dict:
     total = sum(per_kernel.values())
     return {"bytes_per_call": total, "bytes_per_share": total / n_shares,
             "per_kernel_bytes_per_share": {k: v / n_shares for k, v in sorted(per_kernel.items(), key=lambda x: -x[1])},
-            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh via tools/gpu_r04c.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                      "passes over tools/tdec_kbench.py --cts 100000, register-resident tower)"}
+            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh via tools/gpu_r04z.sh at the round-4 head: rocprofv3 --pmc "
+                      "FETCH_SIZE / WRITE_SIZE passes over tools/tdec_kbench.py --cts 100000)"}
 
 
 def fp_count_floor() -> dict:
