@@ -7,7 +7,7 @@ v_mad_u64_u32).
     python tools/fpcount.py run --n-ct 2048       # GPU: counts -> profiles/fpcount.json
 
 `build` compiles every csrc/*.hip with -DHBG_FP_COUNT (bls.h: each fp_mul /
-fp_sqr call adds its active-lane count to a device counter; tdec_kernels.hip:
+fp_sqr call adds 1 per active lane to a device counter; tdec_kernels.hip:
 every launcher closes the previous launch's count) into
 tools/libhbgpu_fpcount.so — a tool build, never the product library.
 `run` loads it (HBG_LIB_PATH), generates the bench's TDec epoch
@@ -32,7 +32,9 @@ LIB = os.path.join(ROOT, "tools", "libhbgpu_fpcount.so")
 def build():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from build_variant import build as bv
-    print(bv("fpcount", ["-DHBG_FP_COUNT"]))
+    # no divergent branch next to the products (bls.h fp_count): each lane adds 1, and the compiler's
+    # wave-aggregating atomic optimizer (which would put the branch back) is off
+    print(bv("fpcount", ["-DHBG_FP_COUNT", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]))
 
 
 def _report(lib) -> dict:

@@ -2,8 +2,11 @@
 """SHA3(V) latency probe: threshold-encrypts `--n` messages of `--len` bytes
 (the configs[4] proposer side: 128 contributions of 1 MiB) `--reps` times;
 run it under `rocprofv3 --kernel-trace --stats` for tdec_v_digest_wave's
-time per launch.  `HBG_SHA3_WAVE64=1` selects the round-3 (lo, hi)-per-lane
-sponge for an A/B in the same library.  The digests are checked against
+time per launch.  In a tool build with the A/B switches
+(`python tools/build_variant.py ab -DHBG_TOOL_AB`, loaded with
+HBG_LIB_PATH=tools/libhbgpu_ab.so) `HBG_SHA3_WAVE64=1` selects the round-3
+(lo, hi)-per-lane sponge and `HBG_SHA3_3STAGE=1` the two-stage theta; the
+product library has no environment switch.  The digests are checked against
 hashlib through W's preimage on the host: every ciphertext must pass the
 device Ciphertext::verify.
 """
