@@ -185,6 +185,7 @@ def cpu_baseline(n_sample: int):
 # v_mad_u64_u32 issue rate — 4.44 cycles per wave-instruction per SIMD at 8
 # waves/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) — at the 2.4 GHz
 # nominal clock on 1,024 SIMDs: 35.4 T lane-MADs/s.
+REALTIME_HZ = 100e6  # s_memrealtime: the constant 100 MHz clock of CDNA3/4
 MADS_PER_FP_MUL = 288
 MAD_PEAK = 256 * 4 * 64 / 4.44 * 2.4e9
 # The issue bound of a whole Fp multiplication: 288 v_mad_u64_u32 + 288
@@ -403,9 +404,9 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             "verify_only": {"achieved": achieved_v / 1e12, "frac": achieved_v / MAD_PEAK,
                             "fp_mul_per_share": per_share_v},
             "traffic": None, "count_source": prof["path"] + " (" + prof.get("source", "") + ")",
-            "count_note": "the combine's count predates its reuse of the verified shares' affine points (no second "
-                          "decompression): ~140 of its 818 Fp ops per share are no longer executed, so the whole-"
-                          "call count is ~2 % high; the instrumented build of HEAD faults (DESIGN.md §5)",
+            "count_note": "counted at this round's kernels by the branch-free instrumented build (one atomic add per "
+                          "active lane per Fp product; DESIGN.md §4 'The HBG_FP_COUNT fault'), outputs checked "
+                          "against the product's",
             "peak_source": "v_mad_u64_u32 4.44 cyc/wave-instr/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) "
                            "x 1024 SIMDs x 64 lanes x 2.4 GHz",
             "note": "each Fp mul also issues 288 v_addc (carry) + ~95 other VALU: frac <= ~0.5 by construction",
@@ -446,6 +447,7 @@ def wire_leg(ctx, dev, n_msgs: int, msg_len: int, reps: int):
     g = torch.Generator(device="cpu").manual_seed(0x5167)
     msgs = torch.randint(0, 256, (n_msgs, msg_len), dtype=torch.uint8, generator=g)
     msgs[:, :4] = torch.tensor([7, 0, 0, 0], dtype=torch.uint8)  # WireMessageKind::Message: poll verifies it
+    msgs[:, 4:12] = torch.tensor([16, 0, 0, 0, 0, 0, 0, 0], dtype=torch.uint8)  # its Uid: a 16-byte uuid
     msgs = msgs.reshape(-1).to(dev)
     off = (torch.arange(n_msgs + 1, dtype=torch.int64) * msg_len).to(dev)
     flen = 4 + 8 + msg_len + 96
@@ -854,6 +856,75 @@ class Legs:
             return None
 
 
+def checks(decode, tdec, cfg1, n128, epoch, bwire, coin, wire) -> dict:
+    """Every correctness verdict the legs computed, first in the line (the
+    driver keeps only the head of a long line)."""
+    def g(d, *path):
+        for k in path:
+            if not isinstance(d, dict):
+                return None
+            d = d.get(k)
+        return d
+    c = {"decode_oracle_match": g(decode, "oracle_match"), "encode_oracle_match": g(decode, "oracle_sample",
+                                                                                   "encode_oracle_match"),
+         "decode_roundtrip_ok": g(decode, "roundtrip_ok"),
+         "tdec_bits_match": g(tdec, "cpu_baseline", "bits_match"),
+         "tdec_plaintexts_match": g(tdec, "cpu_baseline", "plaintexts_match"),
+         "tdec_driver_outcomes_match": g(tdec, "outcomes_match"), "tdec_driver_bits_match": g(tdec, "ok_bits_match"),
+         "tdec_driver_plaintexts_match": g(tdec, "plaintexts_match"),
+         "config1_roundtrip_ok": g(cfg1, "roundtrip_ok"), "n128_roundtrip_ok": g(n128, "roundtrip_ok"),
+         "epoch_all_decrypted_ok": g(epoch, "all_decrypted_ok"), "broadcast_wire_roundtrip_ok": g(bwire, "roundtrip_ok"),
+         "coin_all_ok": g(coin, "all_ok"), "wire_all_verified": g(wire, "all_verified")}
+    vals = [v for v in c.values() if v is not None]
+    c["all_ok"] = bool(vals) and all(bool(v) for v in vals)
+    return c
+
+
+def clock_probe(ctx, step, n_wg: int, dev) -> dict:
+    """Core clock the fused kernel ran at: one extra (untimed) launch with the
+    in-kernel stamps on (hbg_test_set_clock_probe: s_memtime = shader clock,
+    s_memrealtime = 100 MHz constant clock, at every workgroup's entry and
+    exit).  clock = sum of shader-clock ticks / sum of real time over all
+    workgroups, i.e. the average clock a workgroup saw while resident."""
+    from hydrabadger_amd import _lib
+    buf = torch.zeros(n_wg * 4, dtype=torch.int64, device=dev)
+    _lib.check(_lib.lib().hbg_test_set_clock_probe(ctx.h, buf.data_ptr(), n_wg), "clock probe")
+    try:
+        step()
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(_lib.lib().hbg_test_set_clock_probe(ctx.h, None, 0), "clock probe off")
+    c = buf.view(n_wg, 4).cpu().numpy().astype(np.int64)
+    ticks = int((c[:, 1] - c[:, 0]).sum())
+    real = int((c[:, 3] - c[:, 2]).sum())
+    if real <= 0 or ticks <= 0:
+        return {"clock_GHz": None, "note": "no stamps"}
+    span_ms = (int(c[:, 3].max()) - int(c[:, 2].min())) / REALTIME_HZ * 1e3
+    return {"clock_GHz": ticks / (real / REALTIME_HZ) / 1e9, "workgroups": n_wg, "span_ms": span_ms,
+            "mean_workgroup_us": real / n_wg / REALTIME_HZ * 1e6,
+            "source": "s_memtime / s_memrealtime (100 MHz) stamps per workgroup of one untimed launch"}
+
+
+def rbc_oracle_sample(N: int, L: int, shards, levels, pay, present, out, idx) -> dict:
+    """Checker (not the product path, outside every timed region): the C
+    oracle's send_shards and decode_from_shards on sampled instances of the
+    device batch — shards + tree bit-exact, and the 2f-erased decode payload
+    equal to the device's decode output and to the original payload."""
+    from oracle import corc
+    enc_ok = dec_ok = True
+    for k in idx:
+        p = pay[k].cpu().numpy()
+        rs, rl = corc.rbc_encode_merkle(N, p)
+        enc_ok &= bool(np.array_equal(shards[k, :, :L].cpu().numpy(), rs[:, :L]) and
+                       np.array_equal(levels[k].cpu().numpy(), rl))
+        pm = present[k].cpu().numpy()
+        dmg = rs[:, :L].copy()
+        dmg[pm == 0] = 0
+        got = corc.rbc_decode(N, L, dmg, pm, rl[-1].tobytes())
+        dec_ok &= got is not None and got == p.tobytes() and got == out[k, :len(got)].cpu().numpy().tobytes()
+    return {"instances": [int(k) for k in idx], "encode_oracle_match": enc_ok, "decode_oracle_match": dec_ok}
+
+
 def main():
     a = parse()
     legs = set(LEGS) if a.legs == "all" else set(a.legs.split(","))
@@ -927,6 +998,15 @@ def main():
                 "frac": fused_bytes * B / (ms_step * 1e-3) / HBM_PEAK, "alg_bytes_per_instance": fused_bytes},
         "avg_ms": ms_step, "instances_per_launch": B,
     }
+    clk = None
+    try:
+        clk = clock_probe(ctx, step, B, dev)
+        if clk.get("clock_GHz"):
+            roofline["clock_GHz"] = clk["clock_GHz"]
+            roofline["frac_at_measured_clock"] = achieved_ops / (VALU_PEAK * clk["clock_GHz"] / 2.4)
+            roofline["clock"] = clk
+    except Exception as e:  # noqa: BLE001 - the probe is a report, never the line
+        roofline["clock"] = {"error": repr(e)[:200]}
     kernels = {"rbc_encode_merkle_22_42_ms": ms_step,
                "two_launch": {"ms": ms_two, "merkle_build_ms": ms_merkle, "rs_encode_const_22_42_ms": ms_encode,
                               "merkle_build_valu_frac": ops * B / (ms_merkle * 1e-3) / VALU_PEAK,
@@ -955,6 +1035,7 @@ def main():
         dec()
         torch.cuda.synchronize()
         ok = bool((st == 1).all().item()) and bool(torch.equal(out[:, :PAYLOAD], pay[:nd]))
+        sample = rbc_oracle_sample(N_NODES, L, work, levels, pay, present, out, sorted({0, nd // 2, nd - 1}))
         ms_dec = timed(dec, reps)
         # Roofline (DESIGN.md §4 "decode"): exactly Q = 2f rows are rebuilt from
         # the first D present rows, so the coding work is Q x D x L/4 MAC-words,
@@ -966,7 +1047,8 @@ def main():
         achieved = d_ops * nd / (ms_dec * 1e-3)
         tr = decode_pmc_traffic(nd)
         return {"GBps": nd * PAYLOAD / (ms_dec * 1e-3) / 1e9, "ms": ms_dec, "instances": nd,
-                "erased_per_instance": parity, "roundtrip_ok": ok,
+                "erased_per_instance": parity, "roundtrip_ok": ok, "oracle_match": sample["decode_oracle_match"],
+                "oracle_sample": sample,
                 "roofline": {"bound": "valu", "unit": "Tops/s", "achieved": achieved / 1e12,
                              "peak": VALU_PEAK / 1e12, "frac": achieved / VALU_PEAK,
                              "alg_ops_per_instance": d_ops, "alg_bytes_per_instance": d_bytes,
@@ -1022,7 +1104,8 @@ def main():
         line = {
             "metric": BASE["metric"], "value": value, "unit": "GB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic (device SplitMix64, seed 0x48424247)",
+            "vs_baseline": None, "checks": checks(decode, tdec, cfg1, n128, epoch, bwire, coin, wire),
+            "dtype": "u8", "data": "synthetic (device SplitMix64, seed 0x48424247)",
             "config": {"workload": "rbc_encode_merkle: send_shards N=64 f=21 (RS 22+42) 1 MiB payloads",
                        "n_nodes": N_NODES, "f": (N_NODES - 1) // 3, "payload_bytes": PAYLOAD, "shard_len": L,
                        "instances_per_gpu": B, "global_batch": B * world,

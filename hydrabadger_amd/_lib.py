@@ -37,10 +37,12 @@ HBG_E_WIRE_TAG = -31
 HBG_E_WIRE_FRAME = -32
 HBG_E_INVALID_SIGNATURE = -33
 HBG_E_UNKNOWN_PEER = -34
+HBG_E_WIRE_VALUE = -35
 HBG_WIRE_KIND_MESSAGE, HBG_WIRE_KIND_KEYGEN, HBG_WIRE_KIND_MAX = 7, 9, 10
 
 HBG_SHARE_NONE, HBG_SHARE_ACCEPTED, HBG_SHARE_FAULTY, HBG_SHARE_IGNORED, HBG_SHARE_REPEAT = 0, 1, 2, 3, 4
 HBG_ARRIVAL_CIPHERTEXT = 0xFFFFFFFE
+HBG_ARRIVAL_OWN = 0x80000000
 
 HBG_MSG_VALUE, HBG_MSG_ECHO, HBG_MSG_READY, HBG_MSG_CAN_DECODE, HBG_MSG_ECHO_HASH = 0, 1, 2, 3, 4
 
@@ -97,6 +99,7 @@ SIGNATURES = {
     "hbg_test_set_rbc_fused": (_i, [_vp, C.c_int]),
     "hbg_test_set_rs_split": (_i, [_vp, C.c_int]),
     "hbg_test_set_rbc_decode_fused": (_i, [_vp, C.c_int]),
+    "hbg_test_set_clock_probe": (_i, [_vp, _vp, C.c_uint64]),
     "hbg_test_set_latency_lanes": (C.c_uint64, [C.c_uint64]),
 }
 

@@ -41,10 +41,12 @@ def _deps_mtime(src: str) -> float:
     return max(os.path.getmtime(f) for f in _local_includes(src, {src}))
 
 
-def _compile(src: str, force: bool) -> str:
+def _compile(src: str, force: bool) -> tuple:
+    """(object path, whether it was compiled now)."""
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     deps = _deps_mtime(src)
-    if force or not os.path.exists(obj) or os.path.getmtime(obj) < deps:
+    fresh = not force and os.path.exists(obj) and os.path.getmtime(obj) >= deps
+    if not fresh:
         cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -52,7 +54,7 @@ def _compile(src: str, force: bool) -> str:
         # stamp the object with its inputs' time: an edit made while hipcc ran
         # still marks it stale
         os.utime(obj, (deps, deps))
-    return obj
+    return obj, not fresh
 
 
 def build(force: bool = False, jobs: int | None = None) -> str:
@@ -60,8 +62,12 @@ def build(force: bool = False, jobs: int | None = None) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        res = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs = [o for o, _ in res]
+    # objects carry their inputs' time, which can predate the library linked
+    # from their previous version: relink whenever one was compiled now
+    if (force or any(new for _, new in res) or not os.path.exists(LIB)
+            or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs)):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -27,7 +27,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 46;
+constexpr int kNumSlots = 47;
 
 struct Buf {
     void* p = nullptr;
@@ -58,6 +58,9 @@ struct hbg_ctx {
     // hbg_rbc_decode schedule (hbg_test_set_rbc_decode_fused): 0 plan -> coder(s) -> merkle_build, 1 / -1
     // (default) the fused rbc_decode_merkle where it exists ((D, Q) = (22, 42), N = 64)
     int dec_fused = -1;
+    // clock probe of the fused encoder (hbg_test_set_clock_probe): device buffer of clk_cap x 4 u64
+    uint64_t* clk_buf = nullptr;
+    uint64_t clk_cap = 0;
     int32_t* d_err = nullptr;  // sticky device-side argument error (dev_err.h), 0 = none
     hipEvent_t switch_ev = nullptr;  // hbg_set_stream: orders the new stream after the old one
     // a second stream for independent launches inside one call (fork / join by events)
@@ -68,6 +71,15 @@ struct hbg_ctx {
 };
 
 namespace {
+
+// Every C-ABI entry holds the context lock for its whole body and starts with
+// a clear grid-refusal flag (grid.h): a refusal left set by a path that did
+// not go through HBG_TRY can then never turn a later call's runtime
+// hipErrorInvalidConfiguration into HBG_E_ARG.
+struct CtxLock {
+    std::lock_guard<std::mutex> g;
+    explicit CtxLock(hbg_ctx* c) : g(c->mu) { ::hbg::g_grid_refused = false; }
+};
 
 // A batch too large for one grid is refused by the launchers' own guard
 // (grid.h, before anything of the call is enqueued): an argument error.  Any
@@ -304,6 +316,7 @@ const char* hbg_strerror(int code) {
         case HBG_E_WIRE_FRAME: return "FrameLength";
         case HBG_E_INVALID_SIGNATURE: return "InvalidSignature";
         case HBG_E_UNKNOWN_PEER: return "VerificationMessageReceivedUnknownPeer";
+        case HBG_E_WIRE_VALUE: return "InvalidValue";
         default: return "unknown error";
     }
 }
@@ -407,7 +420,7 @@ struct AuxJoin {
 
 int hbg_set_stream(hbg_ctx* c, void* s) {
     if (!c) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     return switch_stream(c, (hipStream_t)s);
 }
 
@@ -415,7 +428,7 @@ int hbg_ctx_device(const hbg_ctx* c) { return c ? c->device : -1; }
 
 int hbg_reset_stream(hbg_ctx* c) {
     if (!c) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     if (switch_stream(c, c->own) == HBG_OK) return HBG_OK;
     // the external stream could not be ordered (e.g. destroyed before the
     // reset): fall back to a device-wide synchronisation, so the context can
@@ -429,7 +442,7 @@ int hbg_reset_stream(hbg_ctx* c) {
 
 int hbg_sync(hbg_ctx* c) {
     if (!c) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     return sync_status(c);
 }
@@ -441,7 +454,7 @@ int hbg_rs_encode(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* shard
     if (L == 0) return HBG_E_EMPTY_SHARD;
     if (stride < L || (n && !shards)) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t N = D + Q;
     if (flags & HBG_DEVICE) {
@@ -465,7 +478,7 @@ int hbg_rs_reconstruct(hbg_ctx* c, uint32_t D, uint32_t Q, uint64_t L, uint8_t* 
     if (L == 0) return HBG_E_EMPTY_SHARD;
     if (stride < L || (n && (!shards || !present))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t N = D + Q;
     if (flags & HBG_DEVICE) {
@@ -493,7 +506,7 @@ int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, 
                      uint64_t n, uint32_t flags) {
     if (!c || N == 0 || N > 256 || stride < L || (n && (!shards || !levels))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t nodes = merkle_nodes(N);
     if (flags & HBG_DEVICE) {
@@ -517,7 +530,7 @@ int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* val
     if (!c || N == 0 || N > 256 || vstride < len || (n && (!values || !index || !ndig || !roots || !ok)))
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t depth = merkle_depth(N);
     if (depth && !digests) return HBG_E_ARG;
@@ -552,7 +565,7 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
     if (!c || N == 0 || N > 256 || L == 0 || stride < L || (n && (!payloads || !plen || !shards || !levels)))
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t Q = 2 * hbg_num_faulty(N), D = N - Q;
     const uint32_t nodes = merkle_nodes(N);
@@ -561,7 +574,8 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
         HBG_TRY(launch_rbc_check_plen(n, dplen, dps, D, L, c->d_err, c->stream));
         const bool fused = c->rbc_fused == 1 || (c->rbc_fused < 0 && D == 22 && Q == 42);
         if (fused && Q && const_encoder_fits(D, Q, S, dps, true)) {  // one launch: encode + leaves + tree
-            HBG_TRY(launch_rbc_encode_merkle(D, Q, dsh, S, L, n, dpay, dps, dplen, dlev, c->stream));
+            HBG_TRY(launch_rbc_encode_merkle(D, Q, dsh, S, L, n, dpay, dps, dplen, dlev, c->stream, c->clk_buf,
+                                             c->clk_cap));
             return HBG_OK;
         }
         if (Q) {
@@ -604,7 +618,7 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
         (n && (!shards || !present || !roots || !out || !plen || !status)))
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t Q = 2 * hbg_num_faulty(N), D = N - Q;
     const uint32_t nodes = merkle_nodes(N);
@@ -747,6 +761,11 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
                           uint32_t n_pk, const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp,
                           const uint32_t* paff, const int32_t* pst, uint8_t* dok,
                           const std::function<int()>& after_leaves = {}, uint32_t* share_aff = nullptr) {
+    if (!share_aff) {  // the leaves' decoded points, re-read by the per-share round (no second decode)
+        void* p;
+        HBG_CHECK(scratch(c, 46, 4ull * bls::kAffWords * n, &p));
+        share_aff = (uint32_t*)p;
+    }
     uint32_t* tbl = nullptr;
     if (c->tdec_batched == 2 || (uint64_t)n >= kPkTableMinUses * n_pk) {
         void* p;
@@ -838,9 +857,10 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_TRY(bls::launch_tdec_batch_check(16 * nb, counts + 2, it2, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok,
                                          nullptr, nullptr, (uint32_t*)fails, counts + 1, c->stream));
     HBG_DBG_STEP(c, "check round 2");
-    // round 3: the shares of failing quads, one by one (the reference's equation)
+    // round 3: the shares of failing quads, one by one (the reference's equation
+    // on the points the leaves decoded)
     HBG_TRY(bls::launch_tdec_verify_shares(n, counts + 1, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff,
-                                           pst, dok, c->stream, (const uint32_t*)fails));
+                                           pst, dok, c->stream, (const uint32_t*)fails, share_aff));
     HBG_DBG_STEP(c, "per-share round");
     return HBG_OK;
 }
@@ -864,7 +884,7 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     if (n == 0) return HBG_OK;
     if (n_ct == 0xFFFFFFFFu || n_pk == 0xFFFFFFFFu) return HBG_E_ARG;  // the sentinels need one more index
     if (!index_ok(flags, share_ct, n, n_ct) || !index_ok(flags, share_pk, n, n_pk)) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     CtTable t;
     const uint8_t* dV;
@@ -923,7 +943,7 @@ int hbg_ct_verify(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* 
     if (!c || (n_ct && (!U48 || !V_off || !W96 || !ok))) return HBG_E_ARG;
     if (n_ct == 0) return HBG_OK;
     if (n_ct == 0xFFFFFFFFu) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     CtTable t;
     const uint8_t* dV;
@@ -949,7 +969,7 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
     if (n_ct == 0) return HBG_OK;
     if (t >= 4096) return HBG_E_ARG;  // far beyond any N <= 65536 network; bounds the per-lane scratch
     if (!grid_fits(n_ct, 64)) return HBG_E_ARG;  // refused before anything is staged or launched
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t m = (uint64_t)t + 1;
     const uint8_t *dsh = share48, *dV = V;
@@ -1032,7 +1052,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     if (t >= n_nodes || n_ct == 0xFFFFFFFFu || n_nodes == 0xFFFFFFFFu) return HBG_E_ARG;
     const uint64_t n = (uint64_t)n_ct * n_nodes, m = (uint64_t)t + 1;
     if (n >= (1ull << 31)) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     CtTable tab;
     const uint8_t* dV;
@@ -1113,7 +1133,7 @@ int hbg_bls_sign(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_t n, con
     if (!c || (n && (!sk32 || !msg_sk || !msg_off || !sig96 || n_sk == 0))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
     if (!index_ok(flags, msg_sk, n, n_sk)) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
     const void *dsk, *dms, *dm, *doff;
@@ -1133,7 +1153,7 @@ int hbg_bls_verify(hbg_ctx* c, uint32_t n_pk, const uint8_t* pk48, uint64_t n, c
     if (!c || (n && (!pk48 || !msg_pk || !msg_off || !sig96 || !ok || n_pk == 0))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
     if (!index_ok(flags, msg_pk, n, n_pk)) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
     const void *dpk, *dmp, *dm, *doff, *dsig;
@@ -1162,7 +1182,7 @@ int hbg_tdec_encrypt(hbg_ctx* c, const uint8_t* pk48, uint64_t n, const uint8_t*
     if (!c || (n && (!pk48 || !r32 || !msg_off || !U48 || !W96))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
     if (!grid_fits((n + 63) / 64, 64)) return HBG_E_ARG;  // refused before anything is staged or launched
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
     if (!(flags & HBG_DEVICE) && mlen && (!msg || !V)) return HBG_E_ARG;
@@ -1195,7 +1215,7 @@ int hbg_tdec_decrypt_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, uint3
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
     if (!index_ok(flags, share_ct, n, n_ct) || !index_ok(flags, share_sk, n, n_sk)) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const void *dU, *dsk, *dsc, *dss;
     void *dsh, *dst, *uaff, *ust;
@@ -1217,7 +1237,7 @@ int hbg_sig_combine(hbg_ctx* c, uint32_t t, uint64_t n, const uint8_t* share96, 
     if (!c || (n && (!share96 || !share_index || !sig96 || !parity || !status))) return HBG_E_ARG;
     if (n == 0) return HBG_OK;
     if (t >= 64) return HBG_E_ARG;  // one 32- or 64-lane group per coin: t + 1 <= 64
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t m = (uint64_t)t + 1;
     const void *dsh, *dix;
@@ -1244,7 +1264,7 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
     if (n == 0) return HBG_OK;
     if (n_doc == 0xFFFFFFFFu || n_pk == 0xFFFFFFFFu) return HBG_E_ARG;  // the sentinels need one more index
     if (!index_ok(flags, share_doc, n, n_doc) || !index_ok(flags, share_pk, n, n_pk)) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t dlen = (flags & HBG_DEVICE) ? 0 : doc_off[n_doc];
     const void *dpk, *dd, *doff, *dsh, *dsd, *dsp;
@@ -1350,7 +1370,7 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
 
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
     if (!c) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     if (on < 0 || on > 3) return HBG_E_ARG;
     c->tdec_batched = on;
     return HBG_OK;
@@ -1358,21 +1378,29 @@ int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {
 
 int hbg_test_set_rs_split(hbg_ctx* c, int on) {
     if (!c || on < -1 || on > 1) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     c->rs_split = on;
     return HBG_OK;
 }
 
 int hbg_test_set_rbc_decode_fused(hbg_ctx* c, int on) {
     if (!c || on < -1 || on > 1) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     c->dec_fused = on;
+    return HBG_OK;
+}
+
+int hbg_test_set_clock_probe(hbg_ctx* c, uint64_t* dev_buf, uint64_t cap_workgroups) {
+    if (!c || (cap_workgroups && !dev_buf)) return HBG_E_ARG;
+    CtxLock g(c);
+    c->clk_buf = cap_workgroups ? dev_buf : nullptr;
+    c->clk_cap = cap_workgroups;
     return HBG_OK;
 }
 
 int hbg_test_set_rbc_fused(hbg_ctx* c, int on) {
     if (!c) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     if (on < -1 || on > 1) return HBG_E_ARG;
     c->rbc_fused = on;
     return HBG_OK;
@@ -1381,7 +1409,7 @@ int hbg_test_set_rbc_fused(hbg_ctx* c, int on) {
 int hbg_test_bls(hbg_ctx* c, int op, uint32_t n, const uint32_t* in, uint32_t in_words, uint32_t* out,
                  uint32_t out_words) {
     if (!c || !in || !out || n == 0) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     void *di, *dout, *dl;
     HBG_CHECK(scratch(c, 0, 4ull * in_words * n, &di));
@@ -1409,7 +1437,7 @@ int hbg_rbc_write_proof_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* 
         (m && (!shards || !levels || !inst || !index || !out || !out_off || n == 0)))
         return HBG_E_ARG;
     if (m == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     if (flags & HBG_DEVICE) {
         if (stride % 16 || !aligned(shards, 16) || !aligned(out, 16)) return HBG_E_ARG;
@@ -1452,7 +1480,7 @@ int hbg_rbc_read_msgs(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* msgs, c
         (m && (!msgs || !msg_off || !tag || !values || !index || !ndig || !roots || !status || (depth && !digests))))
         return HBG_E_ARG;
     if (m == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     if (flags & HBG_DEVICE) {
         if (vstride % 16 || !aligned(values, 16)) return HBG_E_ARG;
@@ -1507,7 +1535,7 @@ int hbg_wire_sign_frames(hbg_ctx* c, uint32_t n_sk, const uint8_t* sk32, uint64_
         }
         if (msg_off[n] && !msg) return HBG_E_ARG;
     }
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t mlen = (flags & HBG_DEVICE) ? 0 : msg_off[n];
     const uint64_t flen = (flags & HBG_DEVICE) ? 0 : frame_off[n] - frame_off[0];
@@ -1548,7 +1576,7 @@ int hbg_wire_verify_frames(hbg_ctx* c, uint32_t n_pk, const uint8_t* pk48, uint6
     if (!(flags & HBG_DEVICE))
         for (uint64_t k = 0; k < n; ++k)
             if (frame_off[k + 1] < frame_off[k]) return HBG_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint64_t flen = (flags & HBG_DEVICE) ? 0 : frame_off[n] - frame_off[0];
     const void *dpk, *dfp, *dfr, *dfo;
@@ -1585,7 +1613,7 @@ int hbg_synth_bytes(hbg_ctx* c, uint32_t tag, uint64_t first, uint64_t nbytes, u
                     uint64_t n, uint32_t flags) {
     if (!c || ostride < nbytes || (n && !out)) return HBG_E_ARG;
     if (n == 0 || nbytes == 0) return HBG_OK;
-    std::lock_guard<std::mutex> g(c->mu);
+    CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     if (flags & HBG_DEVICE) {
         HBG_TRY(launch_synth(tag, first, nbytes, out, ostride, n, c->stream));

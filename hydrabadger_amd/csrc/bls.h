@@ -51,19 +51,108 @@ BD Fp fp_zero() {
 BD Fp fp_one() { return fp_const(kOne); }
 
 // Instrumented builds only (tools/fpcount.py compiles with -DHBG_FP_COUNT):
-// count the Fp multiplications / squarings every kernel executes, per active
-// lane (one wave-aggregated atomic per call), attributed per launch on the
-// host (tdec_kernels.hip HBG_COUNT_MARK).  The product library has no counter.
+// count the Fp multiplications / squarings every kernel executes, attributed
+// per launch on the host (tdec_kernels.hip HBG_COUNT_MARK).  The product
+// library has no counter.  The counter is one atomic add of 1 per active lane
+// per product, with the compiler's wave-aggregating atomic optimizer off
+// (tools/build_variant.py passes -amdgpu-atomic-optimizer-strategy=None): NO
+// divergent branch next to the products.  Round 4's counter (mode 0: one
+// wave-aggregated add by the first active lane, `if (lane == first)`) made
+// the G2 kernels compute wrong points and then fault ("The
+// HBG_FP_COUNT fault"); modes 0 and 4 stay for tools/ctw_probe.py.
 #ifdef HBG_FP_COUNT
 __device__ unsigned long long g_fp_count[2];  // [0] fp_mul, [1] fp_sqr
+#ifndef HBG_FP_COUNT_MODE
+#define HBG_FP_COUNT_MODE 1
+#endif
 __device__ __forceinline__ void fp_count(int which) {
+#if HBG_FP_COUNT_MODE == 1  // every active lane adds 1 (no divergent branch)
+    atomicAdd(&g_fp_count[which], 1ull);
+#else
     const uint64_t m = __builtin_amdgcn_read_exec();
     const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#if HBG_FP_COUNT_MODE == 0  // round 4: one wave-aggregated atomic by the first active lane
     if (lane == (uint32_t)__builtin_ctzll(m)) atomicAdd(&g_fp_count[which], (unsigned long long)__builtin_popcountll(m));
+#else  // mode 4 (diagnostic): the same branch around an empty statement, no memory operation
+    if (lane == (uint32_t)__builtin_ctzll(m)) asm volatile("s_nop 0" ::: "memory");
+#endif
+#endif
 }
 #define HBG_FP_COUNT_CALL(which) fp_count(which)
 #else
 #define HBG_FP_COUNT_CALL(which) ((void)0)
+#endif
+
+// Diagnostic tool builds only (tools/ctw_probe.py, -DHBG_FP_VERIFY): every
+// product is recomputed by a portable CIOS multiplication (compiler code, no
+// asm) and the first mismatch is recorded with its call site.
+#ifdef HBG_FP_VERIFY
+__device__ unsigned long long g_fp_verify[2];  // [0] mismatches, [1] checks
+__device__ uint32_t g_fp_verify_rec[64];       // site, lane, a[12], b[12], asm r[12], ref r[12]
+__device__ __forceinline__ Fp fp_mul_ref(const Fp& a, const Fp& b) {
+    uint32_t t[14];
+#pragma unroll
+    for (int j = 0; j < 14; ++j) t[j] = 0;
+#pragma unroll 1
+    for (int i = 0; i < 12; ++i) {
+        uint64_t C = 0, s;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            s = (uint64_t)t[j] + (uint64_t)a[j] * b[i] + C;
+            t[j] = (uint32_t)s;
+            C = s >> 32;
+        }
+        s = (uint64_t)t[12] + C;
+        t[12] = (uint32_t)s;
+        t[13] = (uint32_t)(s >> 32);
+        const uint32_t m = t[0] * 0xFFFCFFFDu;
+        s = (uint64_t)t[0] + (uint64_t)m * kP[0];
+        C = s >> 32;
+#pragma unroll
+        for (int j = 1; j < 12; ++j) {
+            s = (uint64_t)t[j] + (uint64_t)m * kP[j] + C;
+            t[j - 1] = (uint32_t)s;
+            C = s >> 32;
+        }
+        s = (uint64_t)t[12] + C;
+        t[11] = (uint32_t)s;
+        t[12] = t[13] + (uint32_t)(s >> 32);
+    }
+    Fp r, u;
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) r[j] = t[j];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) u[j] = __builtin_subc(r[j], kP[j], br, &br);
+    const bool sub = t[12] != 0 || br == 0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) r[j] = sub ? u[j] : r[j];
+    return r;
+}
+__device__ __noinline__ void fp_verify(Fp a, Fp b, Fp r, int site) {
+    const Fp ref = fp_mul_ref(a, b);
+    uint32_t d = 0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) d |= ref[j] ^ r[j];
+    atomicAdd(&g_fp_verify[1], 1ull);
+    if (d && atomicAdd(&g_fp_verify[0], 1ull) == 0) {
+        g_fp_verify_rec[0] = (uint32_t)site;
+        g_fp_verify_rec[1] = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) +
+                             64u * (blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u);
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            g_fp_verify_rec[2 + j] = a[j];
+            g_fp_verify_rec[14 + j] = b[j];
+            g_fp_verify_rec[26 + j] = r[j];
+            g_fp_verify_rec[38 + j] = ref[j];
+        }
+    }
+}
+#define HBG_FP_VERIFY_INPUT(name, v) const Fp name = (v)
+#define HBG_FP_VERIFY_CALL(a, b, r) fp_verify((a), (b), (r), __LINE__)
+#else
+#define HBG_FP_VERIFY_INPUT(name, v) ((void)0)
+#define HBG_FP_VERIFY_CALL(a, b, r) ((void)0)
 #endif
 
 // Montgomery products through the fixed-register subroutines: the operands
@@ -72,13 +161,17 @@ __device__ __forceinline__ void fp_count(int which) {
 // identical products may be merged by the compiler).
 BD Fp fp_mul(Fp a, Fp b) {
     HBG_FP_COUNT_CALL(0);
+    HBG_FP_VERIFY_INPUT(a_in, a);
     asm(HBG_FP_SUB_CALL("hbg_fpmul1") : "+{v[0:11]}"(a) : "{v[12:23]}"(b) : HBG_FP_SUB1_CLOBBERS);
+    HBG_FP_VERIFY_CALL(a_in, b, a);
     return a;
 }
 
 BD Fp fp_sqr(Fp a) {
     HBG_FP_COUNT_CALL(1);
+    HBG_FP_VERIFY_INPUT(a_in, a);
     asm(HBG_FP_SUB_CALL("hbg_fpmul1") : "+{v[0:11]}"(a) : "{v[12:23]}"(a) : HBG_FP_SUB1_CLOBBERS);
+    HBG_FP_VERIFY_CALL(a_in, a_in, a);
     return a;
 }
 
@@ -86,10 +179,14 @@ BD Fp fp_sqr(Fp a) {
 BD void fp_mul2(Fp& r0, Fp& r1, Fp a0, Fp b0, Fp a1, Fp b1) {
     HBG_FP_COUNT_CALL(0);
     HBG_FP_COUNT_CALL(0);
+    HBG_FP_VERIFY_INPUT(x0, a0);
+    HBG_FP_VERIFY_INPUT(x1, a1);
     asm(HBG_FP_SUB_CALL("hbg_fpmul2")
         : "+{v[0:11]}"(a0), "+{v[24:35]}"(a1)
         : "{v[12:23]}"(b0), "{v[36:47]}"(b1)
         : HBG_FP_SUB2_CLOBBERS);
+    HBG_FP_VERIFY_CALL(x0, b0, a0);
+    HBG_FP_VERIFY_CALL(x1, b1, a1);
     r0 = a0;
     r1 = a1;
 }
@@ -99,10 +196,16 @@ BD void fp_mul3(Fp& r0, Fp& r1, Fp& r2, Fp a0, Fp b0, Fp a1, Fp b1, Fp a2, Fp b2
     HBG_FP_COUNT_CALL(0);
     HBG_FP_COUNT_CALL(0);
     HBG_FP_COUNT_CALL(0);
+    HBG_FP_VERIFY_INPUT(x0, a0);
+    HBG_FP_VERIFY_INPUT(x1, a1);
+    HBG_FP_VERIFY_INPUT(x2, a2);
     asm(HBG_FP_SUB_CALL("hbg_fpmul3")
         : "+{v[0:11]}"(a0), "+{v[24:35]}"(a1), "+{v[48:59]}"(a2)
         : "{v[12:23]}"(b0), "{v[36:47]}"(b1), "{v[60:71]}"(b2)
         : HBG_FP_SUB3_CLOBBERS);
+    HBG_FP_VERIFY_CALL(x0, b0, a0);
+    HBG_FP_VERIFY_CALL(x1, b1, a1);
+    HBG_FP_VERIFY_CALL(x2, b2, a2);
     r0 = a0;
     r1 = a1;
     r2 = a2;
@@ -646,14 +749,13 @@ BD G1 g1_mul_u64(const Fp& px, const Fp& py, uint64_t k) {
     return r;
 }
 
-// [k]P for a 64-bit scalar, P Jacobian (full additions; k > 0)
+// [k]P for a 64-bit scalar, P Jacobian (X, Y, Z), Z != 0, k > 0: on the
+// isomorphic curve y^2 = x^3 + 4 Z^6 ((x, y) -> (x Z^2, y Z^3); the a = 0
+// formulas never read the constant) P is the affine (X, Y) — mixed additions
+// — and the result (X', Y', Z') maps back as (X', Y', Z' Z)
 BD G1 g1_mul_u64_jac(const G1& p, uint64_t k) {
-    G1 r = {fp_one(), fp_one(), fp_zero()};
-    for (int i = 63; i >= 0; --i) {
-        r = g1_dbl(r);
-        if ((k >> i) & 1ull) r = g1_add(r, p);
-    }
-    return r;
+    const G1 r = g1_mul_u64(p.x, p.y, k);
+    return {r.x, r.y, fp_mul(r.z, p.z)};
 }
 
 // P in G1  <=>  phi(P) == [-x^2] P,  phi(x, y) = (beta x, y)   (Bowe, eprint 2019/814).

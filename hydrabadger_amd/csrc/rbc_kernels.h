@@ -84,9 +84,11 @@ hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint6
                                   const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
 // Fused send_shards (prefix/pad/chunk + Coding::encode + MerkleTree::from_vec)
 // for the (D, Q) with a compile-time coding matrix (has_const_encoder).
+// clk / clk_cap: the clock probe (hbg_test_set_clock_probe): 4 u64 stamps per
+// workgroup when the grid has at most clk_cap workgroups, else none
 hipError_t launch_rbc_encode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                     const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, uint8_t* levels,
-                                    hipStream_t st);
+                                    hipStream_t st, uint64_t* clk = nullptr, uint64_t clk_cap = 0);
 hipError_t launch_pack_rows(uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t rows, uint64_t n,
                             const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, hipStream_t st);
 hipError_t launch_rbc_check_plen(uint64_t n, const uint64_t* plen, uint64_t pstride, uint32_t D, uint64_t L,

@@ -637,8 +637,17 @@ template <int D, int Q>
 __global__ __launch_bounds__((FusedShape<D, Q>::BLK)) __attribute__((amdgpu_waves_per_eu(FusedShape<D, Q>::WPE)))
 void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uint64_t n,
                        const uint8_t* __restrict__ payloads, uint64_t pstride, const uint64_t* __restrict__ plen,
-                       uint8_t* __restrict__ levels) {
+                       uint8_t* __restrict__ levels, uint64_t* __restrict__ clk) {
     using F = FusedShape<D, Q>;
+    // clock probe (hbg_test_set_clock_probe; null in every product call): the
+    // workgroup's shader-clock (s_memtime) and 100 MHz real-time
+    // (s_memrealtime) stamps at entry and exit, so the bench can report the
+    // core clock the kernel actually ran at beside its roofline fraction
+    uint64_t clk_t0 = 0, clk_r0 = 0;
+    if (clk) {  // wave-uniform
+        clk_t0 = __builtin_amdgcn_s_memtime();
+        clk_r0 = __builtin_amdgcn_s_memrealtime();
+    }
     constexpr uint32_t N = F::N, LPI = F::LPI, NODES = F::NODES, R = F::R;
     // LDS: the parity ring [IPB][Q][R] during the sweep, then the tree levels
     __shared__ __attribute__((aligned(16))) uint64_t lds[F::LDS / 8];
@@ -882,6 +891,16 @@ void rbc_encode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
         __syncthreads();
         lbase += cnt;
         cnt = nn;
+    }
+    if (clk) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) {
+            uint64_t* c = clk + 4ull * blockIdx.x;
+            c[0] = clk_t0;
+            c[1] = t1;
+            c[2] = clk_r0;
+            c[3] = r1;
+        }
     }
 }
 
@@ -1325,6 +1344,21 @@ __global__ __launch_bounds__(256) void rbc_glue_copy(const uint8_t* __restrict__
     }
 }
 
+// A NONE instance's payload row is zeroed over the span a decode may have
+// written ([0, D*L)): the fused N = 64 decoder stores the glued bytes before
+// the root comparison, so without this a NONE row would hold bytes that
+// failed authentication.  One workgroup per instance; an OK instance returns
+// at once (include/hbgpu.h, hbg_rbc_decode).
+__global__ __launch_bounds__(256) void rbc_glue_clear(uint64_t n, uint64_t span, const uint8_t* __restrict__ status,
+                                                      uint8_t* __restrict__ out, uint64_t ostride) {
+    const uint64_t inst = blockIdx.x;
+    if (inst >= n || status[inst] == HBG_DECODE_OK) return;
+    uint32_t* row = reinterpret_cast<uint32_t*>(out + inst * ostride);  // ostride % 4 == 0, out 4-aligned
+    const uint64_t words = span / 4;
+    for (uint64_t w = threadIdx.x; w < words; w += 256) row[w] = 0u;
+    for (uint64_t b = words * 4 + threadIdx.x; b < span; b += 256) out[inst * ostride + b] = 0;
+}
+
 // ============================================================== synthetic inputs
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1414,22 +1448,27 @@ hipError_t launch_rs_encode_const(uint32_t D, uint32_t Q, uint8_t* shards, uint6
 
 template <int D, int Q>
 static hipError_t launch_fused(uint8_t* shards, uint64_t S, uint64_t L, uint64_t n, const uint8_t* payloads,
-                               uint64_t pstride, const uint64_t* plen, uint8_t* levels, hipStream_t st) {
+                               uint64_t pstride, const uint64_t* plen, uint8_t* levels, hipStream_t st,
+                               uint64_t* clk, uint64_t clk_cap) {
     using F = FusedShape<D, Q>;
     const uint64_t blocks = (n + F::IPB - 1) / F::IPB;
     HBG_GRID_CHECK(blocks, F::BLK);
+    if (blocks > clk_cap) clk = nullptr;  // the probe buffer holds clk_cap workgroups
     rbc_encode_merkle<D, Q><<<dim3((uint32_t)blocks), dim3(F::BLK), 0, st>>>(shards, S, L, n, payloads, pstride,
-                                                                             plen, levels);
+                                                                             plen, levels, clk);
     return hipGetLastError();
 }
 
 hipError_t launch_rbc_encode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                     const uint8_t* payloads, uint64_t pstride, const uint64_t* plen, uint8_t* levels,
-                                    hipStream_t st) {
-    if (D == 2 && Q == 2) return launch_fused<2, 2>(shards, S, L, n, payloads, pstride, plen, levels, st);
-    if (D == 6 && Q == 10) return launch_fused<6, 10>(shards, S, L, n, payloads, pstride, plen, levels, st);
-    if (D == 22 && Q == 42) return launch_fused<22, 42>(shards, S, L, n, payloads, pstride, plen, levels, st);
-    if (D == 44 && Q == 84) return launch_fused<44, 84>(shards, S, L, n, payloads, pstride, plen, levels, st);
+                                    hipStream_t st, uint64_t* clk, uint64_t clk_cap) {
+    if (D == 2 && Q == 2) return launch_fused<2, 2>(shards, S, L, n, payloads, pstride, plen, levels, st, clk, clk_cap);
+    if (D == 6 && Q == 10)
+        return launch_fused<6, 10>(shards, S, L, n, payloads, pstride, plen, levels, st, clk, clk_cap);
+    if (D == 22 && Q == 42)
+        return launch_fused<22, 42>(shards, S, L, n, payloads, pstride, plen, levels, st, clk, clk_cap);
+    if (D == 44 && Q == 84)
+        return launch_fused<44, 84>(shards, S, L, n, payloads, pstride, plen, levels, st, clk, clk_cap);
     return hipErrorInvalidValue;
 }
 
@@ -1507,6 +1546,10 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
     rbc_glue_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(shards, S, L, N, D, n, levels, nodes,
                                                                             roots, rstatus, plen, status);
     hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    HBG_GRID_CHECK(n, 256);
+    rbc_glue_clear<<<dim3((uint32_t)n), dim3(256), 0, st>>>(n, maxlen, status, out, ostride);
+    e = hipGetLastError();
     if (e != hipSuccess || !copy) return e;
     rbc_glue_copy<<<dim3((uint32_t)(n * bpi)), dim3(256), 0, st>>>(shards, S, L, N, n, bpi, plen, status, out,
                                                                     ostride);

@@ -658,14 +658,12 @@ BD G2 g2_neg(const G2& p) { return {p.x, fp2_neg(p.y), p.z}; }
 BD G2 g2_psi(const G2& p) {
     return {fp2_mul(fp2_conj(p.x), fp2_const(kPsiX)), fp2_mul(fp2_conj(p.y), fp2_const(kPsiY)), fp2_conj(p.z)};
 }
-// [k]P for Jacobian P (full additions)
+// [k]P for Jacobian P = (X, Y, Z), Z != 0: on the isomorphic curve
+// y^2 = x^3 + b' Z^6 ((x, y) -> (x Z^2, y Z^3)) P is the affine (X, Y), so the
+// loop runs mixed additions and the result maps back as (X', Y', Z' Z)
 BD G2 g2_mul_u64_jac(const G2& p, uint64_t k) {
-    G2 r = {fp2_one(), fp2_one(), fp2_zero()};
-    for (int i = 63 - __builtin_clzll(k); i >= 0; --i) {
-        r = g2_dbl(r);
-        if ((k >> i) & 1ull) r = g2_add(r, p);
-    }
-    return r;
+    const G2 r = g2_mul_u64(p.x, p.y, k);
+    return {r.x, r.y, fp2_mul(r.z, p.z)};
 }
 
 BD G2 g2_scale_by_cofactor(const Fp2& px, const Fp2& py) {
@@ -974,8 +972,13 @@ TDEC_WAVE1_KERNEL void tdec_verify_shares(uint64_t cap, const uint32_t* __restri
 #endif
     bool good = ct_status[ct] == 0 && pk_status[pk] == 0;
     G1A s;
-    if (good) good = g1_decompress(share48 + 48ull * k, s, true);
-    if (good && share_aff) store_aff(share_aff + (uint64_t)kAffWords * k, s);
+    if (sel && share_aff) {  // a batched leaf: decoded and subgroup-checked by tdec_batch_leaves, its point stored
+        const uint32_t* sa = share_aff + (uint64_t)kAffWords * k;
+        s = {load_fp(sa), load_fp(sa + 12), sa[24] != 0};
+    } else {
+        if (good) good = g1_decompress(share48 + 48ull * k, s, true);
+        if (good && share_aff) store_aff(share_aff + (uint64_t)kAffWords * k, s);
+    }
     if (good) {
         const uint32_t* pa = pk_aff + 32ull * pk;
         const Fp pkx = load_fp(pa), pky = fp_neg(load_fp(pa + 12));
@@ -1103,22 +1106,29 @@ TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_af
 // -phi(P) = (beta px, -py), so the batch weight r = a + b x^2 (mod r; the
 // 2^64 pairs give 2^64 distinct weights) costs a 32-bit joint double-and-add
 // (branch-free addend select, as g1_mul_fr) instead of a 64-bit one.
+// The three addends P, [x^2]P and both = P + [x^2]P = (X, Y, Z) share one
+// denominator on the isomorphic curve E_Z: y^2 = x^3 + 4 Z^6, reached by
+// (x, y) -> (x Z^2, y Z^3): there both is the affine (X, Y) and P, [x^2]P are
+// (px Z^2, py Z^3), (beta px Z^2, -py Z^3).  The a = 0 doubling and mixed
+// addition formulas never read the curve constant, so the loop runs on E_Z
+// with mixed additions (11 multiplications instead of 16) and the result
+// (X', Y', Z') maps back to E as (X', Y', Z' Z).  Z != 0: (1 + x^2) P != O
+// for P in G1.
 BD G1 g1_mul_ab32(const Fp& px, const Fp& py, uint32_t a, uint32_t b) {
-    const Fp bx = fp_mul(px, fp_const(kBeta)), by = fp_neg(py);
-    const G1 both = g1_add_mixed({px, py, fp_one()}, bx, by);  // P + [x^2]P (never infinity)
+    const G1 both = g1_add_mixed({px, py, fp_one()}, fp_mul(px, fp_const(kBeta)), fp_neg(py));
+    Fp z2 = fp_sqr(both.z), z3, tx, ty;
+    z3 = fp_mul(z2, both.z);
+    fp_mul2(tx, ty, px, z2, py, z3);
+    const Fp ux = fp_mul(tx, fp_const(kBeta)), uy = fp_neg(ty);
     G1 r = {fp_one(), fp_one(), fp_zero()};
 #pragma unroll 1
     for (int bit = 31; bit >= 0; --bit) {
         r = g1_dbl(r);
         const bool ea = (a >> bit) & 1u, eb = (b >> bit) & 1u;
-        G1 t;
-        t.x = ea ? (eb ? both.x : px) : bx;
-        t.y = ea ? (eb ? both.y : py) : by;
-        t.z = (ea && eb) ? both.z : fp_one();
-        const G1 sum = g1_add(r, t);
+        const G1 sum = g1_add_mixed(r, ea ? (eb ? both.x : tx) : ux, ea ? (eb ? both.y : ty) : uy);
         if (ea || eb) r = sum;
     }
-    return r;
+    return {r.x, r.y, fp_mul(r.z, both.z)};
 }
 
 TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_ct,
@@ -1330,7 +1340,9 @@ TDEC_WAVE1_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ c
 //    an invalid ciphertext (Ciphertext::verify false) ends the instance;
 //    start_decryption drops the held shares that fail verification
 //    (UnverifiedDecryptionShareSender: HBG_SHARE_FAULTY), keeps the rest
-//    (HBG_SHARE_ACCEPTED) and try_output fires if more than t are held;
+//    (HBG_SHARE_ACCEPTED), at a validator's marker (HBG_ARRIVAL_OWN | i)
+//    inserts node i's own share (trusted, never verified) and try_output
+//    fires if more than t are held;
 //  * after it, until terminated: an invalid share is a fault, a valid one is
 //    held, a valid one from a held sender is a repeat fault; try_output fires
 //    at t+1 held;
@@ -1359,9 +1371,12 @@ __global__ __launch_bounds__(256) void tdec_select(uint32_t n_ct, uint32_t N, ui
     // the list's end and whether it carries the ciphertext marker
     uint32_t end = len;
     bool marker = false;
+    auto is_marker = [&](uint32_t s) {
+        return s == HBG_ARRIVAL_CIPHERTEXT || ((s & HBG_ARRIVAL_OWN) && (s & ~HBG_ARRIVAL_OWN) < N);
+    };
     for (uint32_t j = 0; j < len; ++j) {
         const uint32_t s = arr ? arr[j] : j;
-        if (s == HBG_ARRIVAL_CIPHERTEXT) {
+        if (is_marker(s)) {
             marker = true;
         } else if (s >= N) {
             end = j;
@@ -1375,21 +1390,30 @@ __global__ __launch_bounds__(256) void tdec_select(uint32_t n_ct, uint32_t N, ui
     if (ct_set && !good_ct) st = HBG_E_INVALID_CIPHERTEXT;
     for (uint32_t j = 0; j < end && st != HBG_E_INVALID_CIPHERTEXT; ++j) {
         const uint32_t s = arr ? arr[j] : j;
-        if (s == HBG_ARRIVAL_CIPHERTEXT) {
+        if (is_marker(s)) {
             if (ct_set) continue;
             ct_set = true;
             if (!good_ct) {
                 st = HBG_E_INVALID_CIPHERTEXT;
                 break;
             }
-            for (uint32_t i = 0; i < N; ++i) {  // start_decryption: node-id order
-                if (!(oc[i] & kPending)) continue;
-                if (ok[k * N + i]) {
+            // start_decryption, node-id order: drop the invalid held shares, then (a
+            // validator, HBG_ARRIVAL_OWN | i) insert its own share — trusted, never
+            // verified — so the first t+1 held by node id are the selection
+            const uint32_t own = s == HBG_ARRIVAL_CIPHERTEXT ? N : (s & ~HBG_ARRIVAL_OWN);
+            for (uint32_t i = 0; i < N; ++i) {
+                bool add = false;
+                if (oc[i] & kPending) {
+                    add = ok[k * N + i] != 0;
+                    oc[i] = (uint8_t)((oc[i] & HBG_SHARE_REPEAT) | (add ? HBG_SHARE_ACCEPTED : HBG_SHARE_FAULTY));
+                }
+                if (i == own) {
+                    add = true;
                     oc[i] = (uint8_t)((oc[i] & HBG_SHARE_REPEAT) | HBG_SHARE_ACCEPTED);
+                }
+                if (add) {
                     if (held < m) idx[held] = i;
                     ++held;
-                } else {
-                    oc[i] = (uint8_t)((oc[i] & HBG_SHARE_REPEAT) | HBG_SHARE_FAULTY);
                 }
             }
             term = held >= m;
@@ -1648,8 +1672,13 @@ BD void split_x2(const uint32_t (&l)[8], uint32_t (&q)[5], uint32_t (&rm)[5]) {
 BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
     uint32_t q[5], rm[5];
     split_x2(l, q, rm);
-    const Fp bx = fp_mul(px, fp_const(kBeta)), by = fp_neg(py);  // [x^2]P
-    const G1 both = g1_add_mixed({px, py, fp_one()}, bx, by);    // P + [x^2]P (never infinity)
+    // P + [x^2]P (never infinity) and the addends on its isomorphic curve E_Z
+    // (g1_mul_ab32): mixed additions only, the result mapped back by Z
+    const G1 both = g1_add_mixed({px, py, fp_one()}, fp_mul(px, fp_const(kBeta)), fp_neg(py));
+    Fp z2 = fp_sqr(both.z), z3, tx, ty;
+    z3 = fp_mul(z2, both.z);
+    fp_mul2(tx, ty, px, z2, py, z3);
+    const Fp ux = fp_mul(tx, fp_const(kBeta)), uy = fp_neg(ty);
     G1 r = {fp_one(), fp_one(), fp_zero()};  // doubling / adding to infinity stays exact
 #pragma unroll
     for (int w = 4; w >= 0; --w) {
@@ -1658,15 +1687,11 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
         for (int bit = (w == 4 ? 0 : 31); bit >= 0; --bit) {
             r = g1_dbl(r);
             const bool a = (rw >> bit) & 1u, b = (qw >> bit) & 1u;
-            G1 t;
-            t.x = a ? (b ? both.x : px) : bx;
-            t.y = a ? (b ? both.y : py) : by;
-            t.z = (a && b) ? both.z : fp_one();
-            const G1 sum = g1_add(r, t);
+            const G1 sum = g1_add_mixed(r, a ? (b ? both.x : tx) : ux, a ? (b ? both.y : ty) : uy);
             if (a || b) r = sum;
         }
     }
-    return r;
+    return {r.x, r.y, fp_mul(r.z, both.z)};
 }
 
 // PublicKeySet::decrypt as a bucket multi-scalar multiplication per G-lane
@@ -1857,6 +1882,9 @@ BD G2 g2_mul_scalar(const Fp2& px, const Fp2& py, const uint32_t (&k)[8]) {
     split_x2(k, q, rm);
     const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));  // [x^2]P, Z = 1
     const G2 both = g2_add_mixed({px, py, fp2_one()}, B.x, B.y);
+    // the addends on the isomorphic curve of both's Z (g1_mul_ab32): mixed additions
+    const Fp2 z2 = fp2_sqr(both.z), z3 = fp2_mul(z2, both.z);
+    const Fp2 tx = fp2_mul(px, z2), ty = fp2_mul(py, z3), ux = fp2_mul(B.x, z2), uy = fp2_mul(B.y, z3);
     G2 r = {fp2_one(), fp2_one(), fp2_zero()};
 #pragma unroll
     for (int w = 4; w >= 0; --w) {
@@ -1865,15 +1893,11 @@ BD G2 g2_mul_scalar(const Fp2& px, const Fp2& py, const uint32_t (&k)[8]) {
         for (int bit = (w == 4 ? 0 : 31); bit >= 0; --bit) {
             r = g2_dbl(r);
             const bool a = (rw >> bit) & 1u, b = (qw >> bit) & 1u;
-            G2 t;
-            t.x = a ? (b ? both.x : px) : B.x;
-            t.y = a ? (b ? both.y : py) : B.y;
-            t.z = (a && b) ? both.z : fp2_one();
-            const G2 sum = g2_add(r, t);
+            const G2 sum = g2_add_mixed(r, a ? (b ? both.x : tx) : ux, a ? (b ? both.y : ty) : uy);
             if (a || b) r = sum;
         }
     }
-    return r;
+    return {r.x, r.y, fp2_mul(r.z, both.z)};
 }
 
 // hash_g2(msg): ChaChaRng seeded with SHA3-256(msg)
@@ -1944,6 +1968,44 @@ __device__ __forceinline__ uint64_t wire_le(const uint8_t* p, int nb) {
     return v;
 }
 
+// poll's bincode::deserialize::<WireMessage> for the two verified kinds, as far
+// as the reference tree defines their fields (oracle/wire.py body_status):
+// Message(Uid, DhbMessage): Uid = u64 length (16) + 16 bytes, then the hbbft
+// message's u32 index; KeyGen(InstanceId {BuiltIn, User(Uid)},
+// key_gen::Message {kind: Part | Ack}) + the first 4 bytes of Part / Ack.
+BD int32_t wire_uid(const uint8_t* m, uint64_t len, uint64_t& p) {
+    if (len < p + 8) return HBG_E_WIRE_EOF;
+    const uint64_t n = wire_le(m + p, 8);
+    p += 8;
+    if (n > len - p) return HBG_E_WIRE_EOF;
+    if (n != 16) return HBG_E_WIRE_VALUE;
+    p += 16;
+    return HBG_OK;
+}
+BD int32_t wire_body_status(const uint8_t* m, uint64_t len) {
+    const uint32_t kind = (uint32_t)wire_le(m, 4);
+    uint64_t p = 4;
+    if (kind == HBG_WIRE_KIND_MESSAGE) {
+        const int32_t st = wire_uid(m, len, p);
+        if (st) return st;
+        return len >= p + 4 ? HBG_OK : HBG_E_WIRE_EOF;
+    }
+    if (kind == HBG_WIRE_KIND_KEYGEN) {
+        if (len < p + 4) return HBG_E_WIRE_EOF;
+        const uint32_t inst = (uint32_t)wire_le(m + p, 4);
+        p += 4;
+        if (inst > 1) return HBG_E_WIRE_TAG;
+        if (inst == 1) {
+            const int32_t st = wire_uid(m, len, p);
+            if (st) return st;
+        }
+        if (len < p + 4) return HBG_E_WIRE_EOF;
+        if ((uint32_t)wire_le(m + p, 4) > 1) return HBG_E_WIRE_TAG;
+        return len >= p + 8 ? HBG_OK : HBG_E_WIRE_EOF;
+    }
+    return HBG_OK;
+}
+
 TDEC_WAVE1_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict__ pk_aff,
                                     const int32_t* __restrict__ pk_status, uint32_t n_pk,
                                     const uint32_t* __restrict__ frame_pk, const uint8_t* __restrict__ frames,
@@ -1968,7 +2030,9 @@ TDEC_WAVE1_KERNEL void wire_verify_frames(uint64_t n, const uint32_t* __restrict
         else {
             const uint32_t kind = (uint32_t)wire_le(f + 12, 4);
             if (kind > HBG_WIRE_KIND_MAX) st = HBG_E_WIRE_TAG;
-            else if (kind == HBG_WIRE_KIND_MESSAGE || kind == HBG_WIRE_KIND_KEYGEN) {
+            else if ((st = wire_body_status(f + 12, mlen)) != HBG_OK) {
+                // Error::Serde: the WireMessage does not deserialise (before any verification)
+            } else if (kind == HBG_WIRE_KIND_MESSAGE || kind == HBG_WIRE_KIND_KEYGEN) {
                 const uint32_t p = frame_pk[k];
                 if (p >= n_pk || pk_status[p] != 0) st = HBG_E_UNKNOWN_PEER;
             }
@@ -2191,23 +2255,23 @@ TDEC_WAVE1_KERNEL void sig_doc_prepare(uint32_t n, const uint8_t* __restrict__ d
 // quad / 16-group / batch sums by cross-lane butterflies.
 // [a]P + [b]psi^2(P) = [a + b x^2]P for P in G2 (affine), 32-bit a, b (psi = [x]
 // on G2; psi^2 of an affine point is affine) — the G2 half of the coin
-// shares' batch weights, same joint double-and-add as g1_mul_ab32.
+// shares' batch weights, same joint double-and-add (and the same mixed
+// additions on the isomorphic curve y^2 = x^3 + b' Z^6 of the common
+// denominator Z of both = P + psi^2(P)) as g1_mul_ab32.
 BD G2 g2_mul_ab32(const Fp2& px, const Fp2& py, uint32_t a, uint32_t b) {
-    const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));
+    const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));  // affine: conj(conj(1)) = 1
     const G2 both = g2_add_mixed({px, py, fp2_one()}, B.x, B.y);
+    const Fp2 z2 = fp2_sqr(both.z), z3 = fp2_mul(z2, both.z);
+    const Fp2 tx = fp2_mul(px, z2), ty = fp2_mul(py, z3), ux = fp2_mul(B.x, z2), uy = fp2_mul(B.y, z3);
     G2 r = {fp2_one(), fp2_one(), fp2_zero()};
 #pragma unroll 1
     for (int bit = 31; bit >= 0; --bit) {
         r = g2_dbl(r);
         const bool ea = (a >> bit) & 1u, eb = (b >> bit) & 1u;
-        G2 t;
-        t.x = ea ? (eb ? both.x : px) : B.x;
-        t.y = ea ? (eb ? both.y : py) : B.y;
-        t.z = (ea && eb) ? both.z : fp2_one();
-        const G2 sum = g2_add(r, t);
+        const G2 sum = g2_add_mixed(r, ea ? (eb ? both.x : tx) : ux, ea ? (eb ? both.y : ty) : uy);
         if (ea || eb) r = sum;
     }
-    return r;
+    return {r.x, r.y, fp2_mul(r.z, both.z)};
 }
 
 TDEC_WAVE1_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_doc,
@@ -2543,11 +2607,21 @@ hipError_t launch_tdec_v_digest(uint64_t n, const uint8_t* V, const uint64_t* V_
     HBG_COUNT_MARK("tdec_v_digest", st);
     if (n == 0) return hipSuccess;
     HBG_GRID_CHECK((n + 63) / 64, 64);
-    static const bool wave64 = std::getenv("HBG_SHA3_WAVE64") != nullptr;  // A/B: the (lo, hi)-per-lane sponge
-    static const bool three_stage = std::getenv("HBG_SHA3_3STAGE") != nullptr;  // A/B: theta in two stages
-    static const uint64_t wave_max = std::getenv("HBG_VDIGEST_WAVE_MAX")  // A/B of the cut
-                                         ? std::strtoull(std::getenv("HBG_VDIGEST_WAVE_MAX"), nullptr, 10)
-                                         : kVDigestWaveMax;
+#ifdef HBG_TOOL_AB
+    // tool builds only (tools/build_variant.py ... -DHBG_TOOL_AB; tools/sha3v_probe.py): A/B switches of
+    // the sponge schedule and of the wave / lane cut, read once per process
+    static const bool wave64 = std::getenv("HBG_SHA3_WAVE64") != nullptr;  // the (lo, hi)-per-lane sponge
+    static const bool three_stage = std::getenv("HBG_SHA3_3STAGE") != nullptr;  // theta in two stages
+    static const uint64_t wave_max = [] {
+        const char* v = std::getenv("HBG_VDIGEST_WAVE_MAX");
+        char* end = nullptr;
+        const unsigned long long x = v ? std::strtoull(v, &end, 10) : 0;
+        return (v && end != v && *end == 0) ? (uint64_t)x : kVDigestWaveMax;  // malformed: the default
+    }();
+#else
+    constexpr bool wave64 = false, three_stage = false;
+    constexpr uint64_t wave_max = kVDigestWaveMax;
+#endif
     if (n <= wave_max && wave64)
         tdec_v_digest_wave64<<<dim3((uint32_t)n), dim3(64), 0, st>>>(n, V, V_off, dig);
     else if (n <= wave_max && three_stage)

@@ -81,11 +81,17 @@ def ct_bytes(contrib_len: int) -> int:
 
 
 def instance_id(epoch: int, p: int) -> int:
+    # bits [0, 20) proposer, [20, 40) epoch; arrival_id puts node + 1 in [40, 48)
+    # and the stream tag sits at bit 48, so every field must stay in its range
+    if not (0 <= p < 1 << 20 and 0 <= epoch < 1 << 20):
+        raise ValueError(f"instance id fields out of range: epoch {epoch}, proposer {p}")
     return (epoch << 20) | p
 
 
 def arrival_id(epoch: int, p: int, node: int = -1) -> int:
     """Seed id of an arrival order: instance p's shared view (node -1) or node `node`'s."""
+    if node >= 255:
+        raise ValueError(f"node {node} does not fit the arrival id's 8-bit node field")
     return instance_id(epoch, p) | (0 if node < 0 else (node + 1) << 40)
 
 
@@ -395,15 +401,28 @@ class HoneyBadgerEpoch:
             silent = np.array([s in faults.silent for s in range(N)])
             order = arrival_orders_views(epoch, acc, N, views, dev)         # [v][k][N]
             keep = ~silent[order]
+            per_node = views[0] >= 0
+            vv = np.array(views, np.int64).reshape(-1, 1, 1)
+            if per_node:  # a node's own share is no network arrival: its start_decryption inserts it
+                keep &= order != vv
             # silent senders' entries dropped, the rest kept in arrival order, -1 padded
             order = np.take_along_axis(order, np.argsort(~keep, axis=-1, kind="stable"), -1)
             order[np.arange(N) >= keep.sum(-1, keepdims=True)] = -1
-            arr = order.astype(np.int32)
+            if per_node:  # hbbft start_decryption at validator v (HBG_ARRIVAL_OWN | v) before any arrival
+                own = np.broadcast_to(np.int64(_lib.HBG_ARRIVAL_OWN) | vv, (nv, k, 1))
+                order = np.concatenate([own, order], -1)
+            arr = order.astype(np.int64).astype(np.uint32).view(np.int32)
             # view v's instance of ciphertext q: its own copy of (U, V, W) and the N shares
+            sh = share48.repeat(nv, 1, 1).view(nv, k, N, 48)
+            for vi, v in enumerate(views):
+                if per_node and v in faults.bad_share:  # it sends a wrong share, but holds its true one
+                    sh[vi, :, v] = e.decrypt_shares(U, self.sk32[v:v + 1].contiguous(),
+                                                    torch.arange(k, dtype=torch.int32, device=dev),
+                                                    torch.zeros(k, dtype=torch.int32, device=dev)).view(k, 48)
             V_off = torch.arange(nv * k + 1, dtype=torch.int64, device=dev) * P
             pt, ct_status, outcome = e.threshold_decrypt(
                 self.t, N, U.repeat(nv, 1), V.repeat(nv, 1).reshape(-1), V_off, W.contiguous().repeat(nv, 1),
-                self.pk48, share48.repeat(nv, 1, 1), torch.from_numpy(arr.reshape(nv * k, N)).to(dev))
+                self.pk48, sh.reshape(nv * k, N, 48), torch.from_numpy(arr.reshape(nv * k, -1)).to(dev))
             plaintexts = pt.view(nv, k, P)
             ct_status = ct_status.view(nv, k)
             outcome = outcome.view(nv, k, N)

@@ -137,6 +137,12 @@ SHARE_NONE, SHARE_ACCEPTED, SHARE_FAULTY, SHARE_IGNORED = (_lib.HBG_SHARE_NONE, 
                                                            _lib.HBG_SHARE_FAULTY, _lib.HBG_SHARE_IGNORED)
 SHARE_REPEAT = _lib.HBG_SHARE_REPEAT  # flag: MultipleDecryptionShares
 ARRIVAL_CIPHERTEXT = _lib.HBG_ARRIVAL_CIPHERTEXT  # arrival entry: set_ciphertext + start_decryption
+ARRIVAL_OWN = _lib.HBG_ARRIVAL_OWN  # ARRIVAL_OWN | i: the same at validator node i (own share inserted)
+
+
+def is_marker(s: int, n: int) -> bool:
+    """An arrival entry at which set_ciphertext + start_decryption run."""
+    return s == ARRIVAL_CIPHERTEXT or (s & ARRIVAL_OWN != 0 and (s & ~ARRIVAL_OWN) < n)
 
 
 def threshold_decrypt_arrays(t: int, n_nodes: int, U, V, V_off, W, pk48, share48, arrival, plaintext, status,
@@ -160,8 +166,10 @@ def threshold_decrypt_batch(t: int, cts: list, pk_shares: list, shares: list, ar
     """One node's ThresholdDecrypt instances for an epoch's ciphertexts:
     shares[k][i] = sender i's 48-B share of cts[k] (None: never sent);
     arrivals[k] = sender ids in arrival order, repeats allowed, with
-    ARRIVAL_CIPHERTEXT where the ciphertext arrives (None: every sender once
-    in node order, after the ciphertext).  Returns (plaintexts (None where
+    ARRIVAL_CIPHERTEXT where the ciphertext arrives at an observer or
+    ARRIVAL_OWN | i where it arrives at validator node i (hbbft
+    start_decryption inserts node i's own share before try_output) (None:
+    every sender once in node order, after the ciphertext).  Returns (plaintexts (None where
     status != 0), status array, outcome [n_ct][N])."""
     n_ct, n = len(cts), len(pk_shares)
     if n_ct == 0:
@@ -172,7 +180,8 @@ def threshold_decrypt_batch(t: int, cts: list, pk_shares: list, shares: list, ar
     sent = []
     for k in range(n_ct):
         order = list(range(n)) if arrivals is None or arrivals[k] is None else list(arrivals[k])
-        sent.append([i for i in order if i == ARRIVAL_CIPHERTEXT or (i < n and shares[k][i] is not None)])
+        end = next((j for j, i in enumerate(order) if i >= n and not is_marker(i, n)), len(order))
+        sent.append([i for i in order[:end] if is_marker(i, n) or shares[k][i] is not None])  # >= n: the list's end
         for i in range(n):
             if shares[k][i] is not None:
                 sh[k, i] = np.frombuffer(bytes(shares[k][i]), np.uint8)

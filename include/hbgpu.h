@@ -73,6 +73,7 @@ extern "C" {
 #define HBG_E_WIRE_FRAME (-32)            /* length-delimited prefix != frame body    */
 #define HBG_E_INVALID_SIGNATURE (-33)     /* hydrabadger Error::InvalidSignature      */
 #define HBG_E_UNKNOWN_PEER (-34)          /* Error::VerificationMessageReceivedUnknownPeer */
+#define HBG_E_WIRE_VALUE (-35)            /* bincode / serde: a field value is invalid (uuid length != 16) */
 
 #define HBG_DEVICE 1u
 #define HBG_ASYNC 2u
@@ -161,10 +162,11 @@ int hbg_rbc_encode_merkle(hbg_ctx *ctx, uint32_t N, const uint8_t *payloads,
  * tree over all N shards, compare with roots[k]; on match glue the first
  * data shards: payload_out + k*payload_stride gets payload_len[k] bytes and
  * status[k] = HBG_DECODE_OK, else status[k] = HBG_DECODE_NONE.
- * payload_stride >= D * shard_len (D = N - 2f data shards).  Bytes of a
- * payload row past payload_len[k], and the whole row of a NONE instance, are
- * unspecified (the fused N = 64 decoder writes the glued bytes while it
- * rebuilds, before the root comparison). */
+ * payload_stride >= D * shard_len (D = N - 2f data shards).  Bytes of an
+ * OK row past payload_len[k] are unspecified (the fused N = 64 decoder writes
+ * the glued bytes while it rebuilds, before the root comparison); the first
+ * D * shard_len bytes of a NONE instance's row are zeroed (both schedules), so
+ * no unauthenticated byte is ever left in payload_out. */
 int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards,
                    uint64_t shard_stride, const uint8_t *present, const uint8_t *roots,
                    uint8_t *payload_out, uint64_t payload_stride, uint64_t *payload_len,
@@ -211,19 +213,21 @@ int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *sha
  * k (hbbft threshold_decrypt.rs [EXT, recalled from upstream], reached from
  * src/hydrabadger/state.rs:486-487) the arrival list arrival[k][0 ..
  * arrival_len) is replayed; it ends at the first entry >= n_nodes other than
- * HBG_ARRIVAL_CIPHERTEXT (arrival == NULL: every sender once, in node order,
- * after the ciphertext):
+ * a ciphertext marker — HBG_ARRIVAL_CIPHERTEXT (an observer) or
+ * HBG_ARRIVAL_OWN | i (validator node i, i < n_nodes) — (arrival == NULL: every
+ * sender once, in node order, after the ciphertext):
  *  - entries before HBG_ARRIVAL_CIPHERTEXT arrived before HoneyBadger output
  *    the ciphertext: handle_message holds the share unverified; a sender
  *    already held is faulted (FaultKind::MultipleDecryptionShares ->
  *    HBG_SHARE_REPEAT flag);
- *  - at HBG_ARRIVAL_CIPHERTEXT (no marker: before the first entry):
- *    set_ciphertext runs Ciphertext::verify — false -> status[k] =
- *    HBG_E_INVALID_CIPHERTEXT and nothing else happens for k; then
- *    start_decryption drops the held shares that fail
- *    PublicKeyShare::verify_decryption_share
+ *  - at the marker (no marker: before the first entry): set_ciphertext runs
+ *    Ciphertext::verify — false -> status[k] = HBG_E_INVALID_CIPHERTEXT and
+ *    nothing else happens for k; then start_decryption drops the held shares
+ *    that fail PublicKeyShare::verify_decryption_share
  *    (FaultKind::UnverifiedDecryptionShareSender -> HBG_SHARE_FAULTY; the
- *    rest HBG_SHARE_ACCEPTED) and try_output runs;
+ *    rest HBG_SHARE_ACCEPTED), a validator (HBG_ARRIVAL_OWN | i) inserts its
+ *    own share share48[k][i] (decrypt_share_no_verify: trusted, never
+ *    verified; HBG_SHARE_ACCEPTED) and try_output runs;
  *  - later entries, until the instance terminates: an invalid share is a
  *    fault (HBG_SHARE_FAULTY), a valid one is held (HBG_SHARE_ACCEPTED), a
  *    valid one from a sender already held is a repeat fault
@@ -246,6 +250,8 @@ int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *sha
 #define HBG_SHARE_IGNORED 3u  /* arrived after termination                              */
 #define HBG_SHARE_REPEAT 4u   /* flag: MultipleDecryptionShares logged for the sender   */
 #define HBG_ARRIVAL_CIPHERTEXT 0xFFFFFFFEu /* arrival entry: set_ciphertext + start_decryption */
+#define HBG_ARRIVAL_OWN 0x80000000u        /* HBG_ARRIVAL_OWN | i: the same at validator node i,
+                                              whose own share is inserted before try_output */
 int hbg_tdec_threshold_decrypt(hbg_ctx *ctx, uint32_t t, uint32_t n_nodes, uint32_t n_ct,
                                const uint8_t *U48, const uint8_t *V, const uint64_t *V_off,
                                const uint8_t *W96, const uint8_t *pk48, const uint8_t *share48,
@@ -413,14 +419,19 @@ int hbg_wire_sign_frames(hbg_ctx *ctx, uint32_t n_sk, const uint8_t *sk32, uint6
  * whose public keys are pk48[frame_pk[k]] (frame_pk[k] >= n_pk: peer key
  * unknown).  status[k] = 0 (the frame yields its WireMessage: verified, or a
  * kind the reference does not verify), HBG_E_WIRE_FRAME, HBG_E_WIRE_EOF,
- * HBG_E_INVALID_POINT (sig does not deserialise), HBG_E_WIRE_TAG (kind > 10),
- * HBG_E_UNKNOWN_PEER or HBG_E_INVALID_SIGNATURE.  The message of frame k is
- * frames[frame_off[k] + 12 ..][..len].  status 0 covers the frame (codec
- * prefix, HBG_WIRE_MAX_FRAME), the SignedWireMessage layout, the signature
- * point and the WireMessageKind index only: poll's bincode deserialisation
- * of the rest of the WireMessage body (src/lib.rs:402-403, Error::Serde on
- * a malformed body) is left to the caller, which must still deserialise
- * the message it dispatches (control plane). */
+ * HBG_E_INVALID_POINT (sig does not deserialise), HBG_E_WIRE_TAG (kind > 10,
+ * or an InstanceId / key_gen::MessageKind index > 1), HBG_E_WIRE_VALUE (a
+ * uuid of length != 16), HBG_E_UNKNOWN_PEER or HBG_E_INVALID_SIGNATURE.  The
+ * message of frame k is frames[frame_off[k] + 12 ..][..len].  As poll
+ * (src/lib.rs:400-416) the WireMessage is deserialised BEFORE the signature
+ * check: for the two verified kinds the body fields the reference tree
+ * defines are checked — Message(Uid, ..): the Uid (serde bytes: u64 length,
+ * which must be 16, then the 16 bytes, src/lib.rs:149) and the variant index
+ * of the hbbft message that follows; KeyGen(InstanceId, key_gen::Message):
+ * InstanceId {BuiltIn, User(Uid)} and key_gen::MessageKind {Part, Ack}
+ * (src/hydrabadger/key_gen.rs:18-33) with its Part / Ack index.  The bodies
+ * inside the unvendored hbbft types (the DHB message, Part, Ack) and the
+ * unverified kinds' bodies (control plane) are the caller's to deserialise. */
 int hbg_wire_verify_frames(hbg_ctx *ctx, uint32_t n_pk, const uint8_t *pk48, uint64_t n,
                            const uint32_t *frame_pk, const uint8_t *frames, const uint64_t *frame_off,
                            int32_t *status, uint32_t flags);

@@ -40,6 +40,13 @@ int hbg_test_set_rs_split(hbg_ctx *ctx, int on);
  * (D, Q) = (22, 42), N = 64 — and the three-launch schedule elsewhere.
  * Identical shards, levels, statuses and payloads. */
 int hbg_test_set_rbc_decode_fused(hbg_ctx *ctx, int on);
+/* Clock probe of the fused send_shards kernel (rbc_encode_merkle): while set,
+ * every hbg_rbc_encode_merkle launch of at most cap_workgroups workgroups
+ * (one per instance at N = 64) writes 4 u64 per workgroup to dev_buf
+ * (device memory): s_memtime (shader clock) at entry and exit, then
+ * s_memrealtime (constant 100 MHz) at entry and exit.  cap_workgroups = 0
+ * turns it off (the default; the product path never sets it). */
+int hbg_test_set_clock_probe(hbg_ctx *ctx, uint64_t *dev_buf, uint64_t cap_workgroups);
 /* The BLS12-381 kernels exist in two builds with identical results: the
  * throughput build (G1 kernels at two waves per SIMD, pairing / G2 kernels at
  * one) and the latency build (every kernel at one wave per SIMD's register

@@ -63,6 +63,10 @@ class Faults:
 
 
 def instance_id(epoch: int, p: int) -> int:
+    # bits [0, 20) proposer, [20, 40) epoch; arrival_id puts node + 1 in [40, 48)
+    # and the stream tag sits at bit 48, so every field must stay in its range
+    if not (0 <= p < 1 << 20 and 0 <= epoch < 1 << 20):
+        raise ValueError(f"instance id fields out of range: epoch {epoch}, proposer {p}")
     return (epoch << 20) | p
 
 
@@ -90,6 +94,8 @@ def encryption_scalar(epoch: int, p: int) -> int:
 
 def arrival_id(epoch: int, p: int, node: int | None = None) -> int:
     """Seed id of an arrival order: instance p's shared view, or node `node`'s."""
+    if node is not None and not 0 <= node < 255:
+        raise ValueError(f"node {node} does not fit the arrival id's 8-bit node field")
     return instance_id(epoch, p) | (0 if node is None else (node + 1) << 40)
 
 
@@ -219,8 +225,17 @@ def run_epoch(N: int, P: int, seed: int = 1, epoch: int = 0, faults: Faults = Fa
                 pt_v.append(None)
                 oc_v.append([T.SHARE_NONE] * N)
                 continue
-            order = [s for s in arrival_order(epoch, p, N, node) if s not in faults.silent]
-            st, pt, oc = T.threshold_decrypt(t, ct, pk_shares, shares[q], order, cache=caches[q])
+            order = [s for s in arrival_order(epoch, p, N, node) if s not in faults.silent and s != node]
+            sh, cache = shares[q], caches[q]
+            if node is not None:
+                # validator `node`: start_decryption (before any arrival) inserts its own share,
+                # decrypt_share_no_verify with its own key — also when it is silent or sends a bad one
+                order = [T.ARRIVAL_OWN | node] + order
+                if node in faults.silent or node in faults.bad_share:
+                    sh = list(sh)
+                    sh[node] = T.decrypt_share(sks[node], ct)
+                    cache = None
+            st, pt, oc = T.threshold_decrypt(t, ct, pk_shares, sh, order, cache=cache)
             st_v.append(st)
             pt_v.append(pt)
             oc_v.append(list(oc))

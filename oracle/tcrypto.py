@@ -224,6 +224,7 @@ def public_key_share(commitment: list, i: int):
 SHARE_NONE, SHARE_ACCEPTED, SHARE_FAULTY, SHARE_IGNORED = 0, 1, 2, 3
 SHARE_REPEAT = 4  # flag: FaultKind::MultipleDecryptionShares logged for the sender
 ARRIVAL_CIPHERTEXT = 0xFFFFFFFE  # arrival entry: set_ciphertext + start_decryption happen here
+ARRIVAL_OWN = 0x80000000  # ARRIVAL_OWN | i: the same at validator node i, which inserts its own share
 E_NOT_ENOUGH_SHARES, E_INVALID_CIPHERTEXT = -20, -23
 
 
@@ -233,9 +234,12 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
     restated.
 
     arrival: sender ids in arrival order (None: 0..N-1 after the ciphertext);
-    the list ends at the first entry >= N other than ARRIVAL_CIPHERTEXT, the
-    point at which HoneyBadger calls set_ciphertext + start_decryption (no
-    marker: before the first arrival).
+    the list ends at the first entry >= N other than a marker.  The marker is
+    the point at which HoneyBadger calls set_ciphertext + start_decryption (no
+    marker: before the first arrival): ARRIVAL_CIPHERTEXT for an observer,
+    ARRIVAL_OWN | i for validator node i, whose start_decryption inserts its
+    own share (decrypt_share_no_verify: trusted, never verified) into the
+    held map AFTER dropping the invalid held shares and BEFORE try_output.
       * handle_message before the ciphertext: the share is held unverified;
         a sender already held is replaced (same bytes here) and faulted
         (MultipleDecryptionShares -> SHARE_REPEAT flag);
@@ -261,8 +265,11 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
         cache = {}
     n = len(pk_shares)
     order = list(range(n)) if arrival is None else list(arrival)
+
+    def is_marker(s):
+        return s == ARRIVAL_CIPHERTEXT or (s & ARRIVAL_OWN and (s & ~ARRIVAL_OWN) < n)
     for j, s in enumerate(order):
-        if s >= n and s != ARRIVAL_CIPHERTEXT:
+        if s >= n and not is_marker(s):
             order = order[:j]
             break
     outcome = [SHARE_NONE] * n
@@ -276,12 +283,12 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
             cache[("v", s)] = shares[s] is not None and verify_decryption_share(pk_shares[s], shares[s], ct, h)
         return cache[("v", s)]
 
-    ct_set = ARRIVAL_CIPHERTEXT not in order
+    ct_set = not any(is_marker(s) for s in order)
     if ct_set and not ct_ok:
         return E_INVALID_CIPHERTEXT, None, outcome
     pending, held, term = set(), set(), False
     for s in order:
-        if s == ARRIVAL_CIPHERTEXT:
+        if is_marker(s):
             if ct_set:
                 continue
             ct_set = True
@@ -294,6 +301,10 @@ def threshold_decrypt(t: int, ct: Ciphertext, pk_shares: list, shares: list, arr
                 else:
                     outcome[p] |= SHARE_FAULTY
             pending.clear()
+            if s != ARRIVAL_CIPHERTEXT:  # our own share: inserted unverified (replacing a held one)
+                own = s & ~ARRIVAL_OWN
+                outcome[own] = (outcome[own] & SHARE_REPEAT) | SHARE_ACCEPTED
+                held.add(own)
             term = len(held) >= t + 1
             continue
         if not ct_set:

@@ -110,7 +110,60 @@ MAX_FRAME = 8 * 1024 * 1024
 E_WIRE_FRAME = -32
 E_INVALID_SIGNATURE = -33
 E_UNKNOWN_PEER = -34
+E_WIRE_VALUE = -35
 E_INVALID_POINT = -22
+INSTANCE_BUILTIN, INSTANCE_USER = 0, 1   # key_gen::InstanceId (src/hydrabadger/key_gen.rs:18-21)
+KEYGEN_PART, KEYGEN_ACK = 0, 1           # key_gen::MessageKind (src/hydrabadger/key_gen.rs:25-28)
+
+
+def _uid(m: bytes, p: int):
+    """serde of hydrabadger's Uid(Uuid) (src/lib.rs:149; uuid 0.6, non-human-
+    readable: serialize_bytes) under bincode: u64 length, the bytes; the uuid
+    visitor rejects a length != 16 (after bincode has read the bytes)."""
+    if len(m) < p + 8:
+        return E_WIRE_EOF, p
+    (n,) = struct.unpack_from("<Q", m, p)
+    p += 8
+    if n > len(m) - p:
+        return E_WIRE_EOF, p
+    if n != 16:
+        return E_WIRE_VALUE, p
+    return OK, p + 16
+
+
+def body_status(message: bytes) -> int:
+    """bincode::deserialize::<WireMessage>(message) (src/lib.rs:402-403) for the
+    two verified kinds, as far as the reference tree defines their fields:
+    Message(Uid, DhbMessage) — the Uid, then the (unvendored) hbbft message's
+    u32 variant index must be present; KeyGen(InstanceId, key_gen::Message) —
+    InstanceId (BuiltIn | User(Uid)), then MessageKind (Part | Ack) and the
+    4 bytes of the first field of Part / Ack.  Unverified kinds: the index only."""
+    m = bytes(message)
+    (kind,) = struct.unpack_from("<I", m, 0)
+    p = 4
+    if kind == KIND_MESSAGE:
+        st, p = _uid(m, p)
+        if st:
+            return st
+        return OK if len(m) >= p + 4 else E_WIRE_EOF
+    if kind == KIND_KEYGEN:
+        if len(m) < p + 4:
+            return E_WIRE_EOF
+        (inst,) = struct.unpack_from("<I", m, p)
+        p += 4
+        if inst > INSTANCE_USER:
+            return E_WIRE_TAG
+        if inst == INSTANCE_USER:
+            st, p = _uid(m, p)
+            if st:
+                return st
+        if len(m) < p + 4:
+            return E_WIRE_EOF
+        (mk,) = struct.unpack_from("<I", m, p)
+        if mk > KEYGEN_ACK:
+            return E_WIRE_TAG
+        return OK if len(m) >= p + 8 else E_WIRE_EOF
+    return OK
 
 
 def frame_len(msg_len: int) -> int:
@@ -149,6 +202,9 @@ def poll_frame(frame: bytes, peer_pk=None) -> int:
     (kind,) = struct.unpack_from("<I", message, 0)
     if kind > KIND_MAX:
         return E_WIRE_TAG
+    st = body_status(message)  # poll deserialises the whole WireMessage before verifying
+    if st:
+        return st
     if kind in (KIND_MESSAGE, KIND_KEYGEN):
         if peer_pk is None:
             return E_UNKNOWN_PEER

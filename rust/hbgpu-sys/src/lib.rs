@@ -37,6 +37,7 @@ pub const HBG_E_WIRE_TAG: c_int = -31;
 pub const HBG_E_WIRE_FRAME: c_int = -32;
 pub const HBG_E_INVALID_SIGNATURE: c_int = -33;
 pub const HBG_E_UNKNOWN_PEER: c_int = -34;
+pub const HBG_E_WIRE_VALUE: c_int = -35;
 
 pub const HBG_DEVICE: u32 = 1;
 pub const HBG_ASYNC: u32 = 2;
@@ -48,6 +49,7 @@ pub const HBG_SHARE_FAULTY: u8 = 2;
 pub const HBG_SHARE_IGNORED: u8 = 3;
 pub const HBG_SHARE_REPEAT: u8 = 4;
 pub const HBG_ARRIVAL_CIPHERTEXT: u32 = 0xFFFF_FFFE;
+pub const HBG_ARRIVAL_OWN: u32 = 0x8000_0000;
 pub const HBG_MSG_VALUE: u32 = 0;
 pub const HBG_MSG_ECHO: u32 = 1;
 pub const HBG_MSG_READY: u32 = 2;

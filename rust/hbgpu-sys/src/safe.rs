@@ -171,8 +171,10 @@ impl Engine {
     /// hbbft ThresholdDecrypt for an epoch (hbg_tdec_threshold_decrypt):
     /// `cts[k] = (U48, V, W96)`, `shares[k][i]` = sender i's share of ct k
     /// (None: never arrived), `arrival[k]` = sender order, repeats allowed,
-    /// with `HBG_ARRIVAL_CIPHERTEXT` where the ciphertext arrives (None: node
-    /// order, after the ciphertext).  Returns per ciphertext `Ok(plaintext)`
+    /// with `HBG_ARRIVAL_CIPHERTEXT` where the ciphertext arrives at an
+    /// observer, or `HBG_ARRIVAL_OWN | i` where it arrives at validator node i
+    /// (its own share is inserted before try_output) (None: node order,
+    /// after the ciphertext).  Returns per ciphertext `Ok(plaintext)`
     /// or the status code, and the per-sender outcomes (HBG_SHARE_*, possibly
     /// | HBG_SHARE_REPEAT).
     #[allow(clippy::type_complexity)]
@@ -204,8 +206,12 @@ impl Engine {
                     sh[48 * (k * n + i)..48 * (k * n + i + 1)].copy_from_slice(x);
                 }
             }
+            let marker = |s: u32| s == HBG_ARRIVAL_CIPHERTEXT
+                || (s & HBG_ARRIVAL_OWN != 0 && ((s & !HBG_ARRIVAL_OWN) as usize) < n);
+            // an entry >= n that is no marker ends the list
             sent.push(order.into_iter()
-                .filter(|&s| s == HBG_ARRIVAL_CIPHERTEXT || ((s as usize) < n && shares[k][s as usize].is_some()))
+                .take_while(|&s| marker(s) || (s as usize) < n)
+                .filter(|&s| marker(s) || shares[k][s as usize].is_some())
                 .collect());
         }
         let alen = sent.iter().map(|o| o.len() + 1).max().unwrap_or(1);

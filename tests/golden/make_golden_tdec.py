@@ -33,26 +33,27 @@ def a18_cases():
     """hbbft ThresholdDecrypt arrival cases on the N=7 scenario (SURVEY.md §8
     a18), seen from node 0: `crate_arrival` is what hbbft's ThresholdDecrypt
     of node 0 receives (handle_message per entry, "ct" = set_ciphertext +
-    start_decryption, which holds node 0's own share; no "ct": before the
-    first entry); `arrival` is the same history for hbg_tdec_threshold_decrypt,
-    where node 0's share is an ordinary arrival right after the ciphertext.
-    The two agree while fewer than t+1 shares are held at the ciphertext (true
-    for every case here).  One share replaced by a bad one (`bad_sender`);
-    status / outcomes / plaintext are the oracle's."""
+    start_decryption, which inserts node 0's own share before try_output; no
+    "ct": before the first entry); `arrival` is the same history for
+    hbg_tdec_threshold_decrypt, whose marker for a validator is
+    ARRIVAL_OWN | 0 ("own").  The last case holds t+1 valid shares at the
+    ciphertext already: node 0's own share is among the first t+1 by node id
+    (accepted and interpolated) as in hbbft.  One share replaced by a bad one
+    (`bad_sender`); status / outcomes / plaintext are the oracle's."""
     s = scenario(7, 3, 40, 1)
     t, pks = s["t"], s["pk_shares"]
     M = T.ARRIVAL_CIPHERTEXT
     cases = []
+    OWN0 = T.ARRIVAL_OWN | 0
     for k, bad, crate in ((0, 1, [6, 6, 1, 5, 3, 2]), (1, 1, [3, 1, 3, M, 2, 4]), (2, 4, [5, 4, 6, M, 1, 2]),
-                          (0, 1, [1, M, 1, 2]), (1, 2, [1, 2, 2, 3, 4, 5, 6])):
-        arrival = list(crate)
-        arrival.insert(crate.index(M) + 1 if M in crate else 0, 0)
+                          (0, 1, [1, M, 1, 2]), (1, 2, [1, 2, 2, 3, 4, 5, 6]), (2, 4, [3, 5, 6, 4, M, 1, 2])):
+        arrival = [OWN0 if a == M else a for a in crate] if M in crate else [OWN0] + list(crate)
         shares = list(s["shares"][k])
         shares[bad] = B.g1_add(shares[bad], B.G1)
         st, pt, oc = T.threshold_decrypt(t, s["cts"][k], pks, shares, arrival)
         cases.append({"ct": k, "bad_sender": bad, "bad_share": B.g1_compress(shares[bad]).hex(),
                       "crate_arrival": ["ct" if a == M else a for a in crate],
-                      "arrival": ["ct" if a == M else a for a in arrival], "status": st,
+                      "arrival": ["own" if a == OWN0 else a for a in arrival], "status": st,
                       "outcome": oc, "plaintext": None if pt is None else pt.hex()})
     return {"outcome_codes": {"none": T.SHARE_NONE, "accepted": T.SHARE_ACCEPTED, "faulty": T.SHARE_FAULTY,
                               "ignored": T.SHARE_IGNORED, "repeat_flag": T.SHARE_REPEAT},

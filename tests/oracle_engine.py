@@ -143,7 +143,7 @@ class OracleEngine:
             except ValueError:
                 st[q] = T.E_INVALID_CIPHERTEXT
                 continue
-            order = [int(s) for s in arrival[q].tolist() if 0 <= int(s) < N]
+            order = [int(s) & 0xFFFFFFFF for s in arrival[q].tolist()]  # u32 entries: markers, -1 ends
             shares = []
             for s in range(N):
                 try:

@@ -100,8 +100,10 @@ def test_oracle_epoch_fault_semantics():
         for q, p in enumerate(out.accepted):
             if p != 6:
                 assert out.ct_status[v][q] == 0
-                assert out.share_outcome[v][q][3] == 0      # silent: no share
-                assert out.share_outcome[v][q][5] in (0, 2, 3)  # bad share: fault if processed, never accepted
+                # silent: no share, except in its own view (start_decryption inserts the own share)
+                assert out.share_outcome[v][q][3] == (1 if v == 3 else 0)
+                # bad share: fault if processed, never accepted — except its own (true) share in its own view
+                assert out.share_outcome[v][q][5] in ((1,) if v == 5 else (0, 2, 3))
 
 
 # ----------------------------------------------------------------------------- product orchestration on CPU

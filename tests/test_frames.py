@@ -21,7 +21,8 @@ from oracle import wire
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "frames_golden.json")))
 UNMUTATED = {"message_ok", "keygen_ok", "message_wrong_key", "goodbye_wrong_key_exempt", "network_state_exempt",
-             "message_unknown_peer", "bad_kind", "short_message", "empty_message"}
+             "message_unknown_peer", "bad_kind", "short_message", "empty_message", "message_bad_uid_len",
+             "keygen_bad_instance_id", "message_truncated_body"}
 
 
 def _sks():
@@ -55,6 +56,32 @@ def test_abi_frame_len_and_errors():
         assert l.hbg_wire_frame_len(n) == wire.frame_len(n)
     assert l.hbg_strerror(_lib.HBG_E_INVALID_SIGNATURE) == b"InvalidSignature"
     assert l.hbg_strerror(_lib.HBG_E_UNKNOWN_PEER) == b"VerificationMessageReceivedUnknownPeer"
+    assert l.hbg_strerror(_lib.HBG_E_WIRE_VALUE) == b"InvalidValue"
+
+
+def test_oracle_body_gate():
+    """poll deserialises the WireMessage before verifying (src/lib.rs:400-416):
+    the fields the reference tree defines for the verified kinds — Message's
+    Uid (uuid: u64 length 16 + 16 bytes), KeyGen's InstanceId and
+    key_gen::MessageKind (src/hydrabadger/key_gen.rs:18-33) — and the index
+    of the hbbft body that follows; unverified kinds: the kind index only."""
+    u = struct.pack("<Q", 16) + bytes(range(16))
+    P = struct.pack
+    assert wire.body_status(P("<I", 7) + u + P("<I", 0)) == wire.OK
+    assert wire.body_status(P("<I", 7) + u + b"\0\0\0") == wire.E_WIRE_EOF       # the hbbft index cut short
+    assert wire.body_status(P("<I", 7) + P("<Q", 15) + bytes(15) + bytes(8)) == wire.E_WIRE_VALUE
+    assert wire.body_status(P("<I", 7) + P("<Q", 17) + bytes(17) + bytes(8)) == wire.E_WIRE_VALUE
+    assert wire.body_status(P("<I", 7) + P("<Q", 1 << 40) + bytes(40)) == wire.E_WIRE_EOF  # bytes past the end
+    assert wire.body_status(P("<I", 7) + bytes(7)) == wire.E_WIRE_EOF
+    assert wire.body_status(P("<II", 9, 0) + P("<I", 1) + bytes(4)) == wire.OK      # BuiltIn, Ack
+    assert wire.body_status(P("<II", 9, 1) + u + P("<I", 0) + bytes(4)) == wire.OK  # User(Uid), Part
+    assert wire.body_status(P("<II", 9, 2) + bytes(40)) == wire.E_WIRE_TAG          # InstanceId index 2
+    assert wire.body_status(P("<II", 9, 0) + P("<I", 2) + bytes(4)) == wire.E_WIRE_TAG  # MessageKind index 2
+    assert wire.body_status(P("<II", 9, 0) + P("<I", 1)) == wire.E_WIRE_EOF
+    assert wire.body_status(P("<I", 5)) == wire.OK                                   # Goodbye: no fields
+    # the gate runs before the signature / peer checks: an unknown peer with a bad body is a Serde error
+    f = wire.signed_frame(P("<IQ", 7, 3) + bytes(40), B.g2_compress(B.G2))
+    assert wire.poll_frame(f, None) == wire.E_WIRE_VALUE
 
 
 # ------------------------------------------------------------------ GPU (C ABI)
@@ -106,6 +133,7 @@ def test_gpu_device_batch_sign_poll():
     sks = [(0x9E3779B97F4A7C15 * (i + 1)) % B.R for i in range(n_sk)]
     msgs = np.frombuffer(synth.synth_bytes(9, 3, n * ln), np.uint8).copy().reshape(n, ln)
     msgs[:, :4] = np.frombuffer(struct.pack("<I", wire.KIND_MESSAGE), np.uint8)
+    msgs[:, 4:12] = np.frombuffer(struct.pack("<Q", 16), np.uint8)  # Message(Uid, ..): a 16-byte uuid
     msg_sk = (np.arange(n) % n_sk).astype(np.uint32)
     moff = np.arange(n + 1, dtype=np.uint64) * ln
     foff = np.arange(n + 1, dtype=np.uint64) * wire.frame_len(ln)
@@ -117,7 +145,7 @@ def test_gpu_device_batch_sign_poll():
     torch.cuda.synchronize()
     bad = np.arange(7, n, 100)
     for k in bad:
-        frames[int(foff[k]) + 12 + 4 + (k % 200)] ^= 1
+        frames[int(foff[k]) + 12 + 4 + 24 + (k % 200)] ^= 1  # in the body past kind + Uid: still deserialises
     all_pk = np.frombuffer(b"".join(B.g1_compress(B.g1_mul(B.G1, k)) for k in sks), np.uint8).copy().reshape(n_sk, 48)
     st = torch.empty(n, dtype=torch.int32, device=dev)
     hw.poll_frames_batch(d(all_pk), d(msg_sk), frames, d(foff), st, device=True)

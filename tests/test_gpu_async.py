@@ -250,7 +250,8 @@ def test_frames_over_the_codec_limit():
     from hydrabadger_amd import _lib
     from hydrabadger_amd import wire as hw
     limit = owire.MAX_FRAME
-    big = struct.pack("<I", owire.KIND_MESSAGE) + bytes(limit - 8 - 96 - 4 + 1)     # body = limit + 1
+    uid = struct.pack("<Q", 16) + bytes(range(16))                                  # Message(Uid, ..): a valid Uid
+    big = struct.pack("<I", owire.KIND_MESSAGE) + uid + bytes(limit - 8 - 96 - 4 - 24 + 1)  # body = limit + 1
     with pytest.raises(_lib.HbgError) as e:
         hw.sign_frames([5], [(0, big)])
     assert e.value.code == _lib.HBG_E_WIRE_FRAME

@@ -77,6 +77,34 @@ def test_oracle_shares_before_the_ciphertext():
     assert st == T.E_NOT_ENOUGH_SHARES and oc == [ACC, FLT, ACC, NONE, NONE, NONE, NONE]
 
 
+def test_oracle_own_share_at_start_decryption():
+    """A validator's start_decryption (ARRIVAL_OWN | i) inserts its own share
+    after dropping the invalid held shares and BEFORE try_output (hbbft
+    threshold_decrypt.rs, via state.rs:486-487): with t+1 valid shares already
+    held at the ciphertext the own share is still accepted and, being among
+    the first t+1 by node id, interpolated; it is never verified."""
+    sc = _case()
+    t, ct, pks = sc["t"], sc["cts"][2], sc["pk_shares"]
+    shares = list(sc["shares"][2])
+    shares[4] = B.g1_add(shares[4], B.G1)
+    M, OWN = T.ARRIVAL_CIPHERTEXT, T.ARRIVAL_OWN
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[3, 5, 6, 4, OWN | 0, 1, 2])
+    assert st == 0 and pt == sc["msgs"][2]
+    assert oc == [ACC, IGN, IGN, ACC, FLT, ACC, ACC]
+    # the observer's marker at the same point: output at the marker from 3, 5, 6; 0 never arrives
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[3, 5, 6, 4, M, 1, 2])
+    assert st == 0 and pt == sc["msgs"][2] and oc == [NONE, IGN, IGN, ACC, FLT, ACC, ACC]
+    # no marker before it: start_decryption (own share first) precedes every arrival
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[OWN | 6, 4, 5, 1])
+    assert st == 0 and oc == [NONE, ACC, NONE, NONE, FLT, ACC, ACC]
+    # the own share is trusted: an invalid own share is inserted unverified (and the output is garbage)
+    st, pt, oc = T.threshold_decrypt(t, ct, pks, shares, arrival=[OWN | 4, 0, 1])
+    assert st == 0 and oc[4] == ACC and pt != sc["msgs"][2]
+    # an own marker with an index >= N ends the list like any other entry >= N
+    assert T.threshold_decrypt(t, ct, pks, shares, arrival=[0, 1, OWN | 7, 2]) == \
+        T.threshold_decrypt(t, ct, pks, shares, arrival=[0, 1])
+
+
 def test_oracle_not_enough_and_invalid_ciphertext():
     sc = _case()
     t, ct, pks = sc["t"], sc["cts"][1], sc["pk_shares"]
@@ -117,8 +145,15 @@ def test_gpu_glue_matches_oracle_hand_cases():
     M = T.ARRIVAL_CIPHERTEXT
     cts += [ct0, ct0, bad_ct, ct1]
     sh += [list(sh[1]), list(sh[1]), list(sc["shares"][2]), list(sc["shares"][1])]
+    O = T.ARRIVAL_OWN
     arrivals = [None, [6, 6, 1, 5, 0, 3, 2], [0, 4], None,
                 [3, 1, 3, M, 0, 2, 4], [5, 4, 6, 0, M, 1, 2], [0, 0, M, 2, 3], [1, 0, 1, M, 1, 2, 2, 5]]
+    # validator markers: own share inserted at start_decryption (also with t+1 already held; an own
+    # index past N ends the list; an invalid own share is trusted)
+    cts += [ct0, ct1, ct2, ct0, ct1]
+    sh += [list(sc["shares"][0]), list(sc["shares"][1]), list(sc["shares"][2]), list(sh[1]), list(sh[1])]
+    arrivals += [[3, 5, 6, 4, O | 0, 1, 2], [O | 6, 4, 5, 1], [5, 4, 6, 0, O | 2, 1], [0, 2, O | 1, 3],
+                 [1, O | 7, 2, 3]]
     pts, st, oc = th.threshold_decrypt_batch(
         t, [th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W)) for c in cts], pks,
         [[B.g1_compress(x) for x in row] for row in sh], arrivals)
@@ -336,7 +371,8 @@ def _a18_fixture():
         ct = sc["cts"][c["ct"]]
         shares = [bytes.fromhex(x) for x in ct["shares"]]
         shares[c["bad_sender"]] = bytes.fromhex(c["bad_share"])
-        arrival = [M if a == "ct" else a for a in c["arrival"]]
+        own = T.ARRIVAL_OWN | g["threshold_decrypt"]["our_node"]
+        arrival = [own if a == "own" else (M if a == "ct" else a) for a in c["arrival"]]
         cases.append((ct, shares, arrival, c))
     return sc, cases
 
