@@ -838,10 +838,76 @@ static_assert(kMillerSqr.w[2] >> 3 == 0, "68 lines: f^2 never follows the last o
 // (c2 Z^3 + c1 XZ + c0 Y), an Fp factor that the final exponentiation maps
 // to 1 ((p - 1) divides (p^12 - 1) / r) — no inversion for a conversion to
 // affine.  Otherwise (a, b) = affine (x, y) and z is unused.
+//
+// The accumulator f lives in LDS, not in registers: 72 u64 words per lane,
+// word w of lane l at f[64 w + l] (a wave's ds_read_b64 of one word is 512
+// contiguous bytes: conflict-free), 36 KiB per one-wave workgroup, so four
+// such waves per CU fit in its 160 KiB.  A line evaluation or a squaring
+// reads the halves it needs when it needs them (a compiler fence between the
+// phases forces the re-read instead of keeping a loaded half live), so at
+// most ~3 Fp6 plus the multiplication window are in registers.  With f in
+// registers (round 4) the 144 words of f beside those temporaries overflowed
+// 256 VGPRs + 256 AGPRs: ~5 KB of scratch reloads per Miller step per lane,
+// ~450 KB per pairing check (profiles/r05 PMC), the pairing kernels' traffic.
+BD void lds_fence() { asm volatile("" ::: "memory"); }
+BD Fp lds_fp(const uint64_t* f, int i) {
+    Fp r;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint64_t v = f[64 * (6 * i + k)];
+        r[2 * k] = (uint32_t)v;
+        r[2 * k + 1] = (uint32_t)(v >> 32);
+    }
+    return r;
+}
+BD void lds_st_fp(uint64_t* f, int i, const Fp& a) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) f[64 * (6 * i + k)] = (uint64_t)a[2 * k] | ((uint64_t)a[2 * k + 1] << 32);
+}
+BD Fp6 lds_fp6(const uint64_t* f, int h) {
+    return {{lds_fp(f, 6 * h), lds_fp(f, 6 * h + 1)},
+            {lds_fp(f, 6 * h + 2), lds_fp(f, 6 * h + 3)},
+            {lds_fp(f, 6 * h + 4), lds_fp(f, 6 * h + 5)}};
+}
+BD void lds_st_fp6(uint64_t* f, int h, const Fp6& a) {
+    lds_st_fp(f, 6 * h, a.c0.c0);
+    lds_st_fp(f, 6 * h + 1, a.c0.c1);
+    lds_st_fp(f, 6 * h + 2, a.c1.c0);
+    lds_st_fp(f, 6 * h + 3, a.c1.c1);
+    lds_st_fp(f, 6 * h + 4, a.c2.c0);
+    lds_st_fp(f, 6 * h + 5, a.c2.c1);
+}
+// f *= (c0 + c1 v + c4 v w): fp12_mul_by_014_v on the LDS accumulator
+BD void lds_mul_by_014(uint64_t* f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
+    const Fp6 aa = fp6_mul_by_01(lds_fp6(f, 0), c0, c1);
+    lds_fence();
+    const Fp6 bb = fp6_mul_by_1(lds_fp6(f, 1), c4);
+    lds_fence();
+    const Fp6 t = fp6_mul_by_01(fp6_add(lds_fp6(f, 1), lds_fp6(f, 0)), c0, fp2_add(c1, c4));
+    lds_fence();
+    lds_st_fp6(f, 1, fp6_sub(fp6_sub(t, aa), bb));
+    lds_st_fp6(f, 0, fp6_add(fp6_mul_by_v(bb), aa));
+    lds_fence();
+}
+// f = f^2: fp12_sqr_v on the LDS accumulator
+BD void lds_sqr(uint64_t* f) {
+    const Fp6 ab = fp6_mul(lds_fp6(f, 0), lds_fp6(f, 1));
+    lds_fence();
+    const Fp6 s = fp6_mul(fp6_add(fp6_mul_by_v(lds_fp6(f, 1)), lds_fp6(f, 0)), fp6_add(lds_fp6(f, 0), lds_fp6(f, 1)));
+    lds_fence();
+    lds_st_fp6(f, 0, fp6_sub(fp6_sub(s, ab), fp6_mul_by_v(ab)));
+    lds_st_fp6(f, 1, fp6_add(ab, ab));
+    lds_fence();
+}
+
 template <bool JAC>
 BD Fp12 miller_loop2(const uint32_t* c1, const Fp& a1, const Fp& b1, const Fp& z1, bool use1, const uint32_t* c2,
                      const Fp& a2, const Fp& b2, const Fp& z2, bool use2) {
-    Fp12 f = fp12_one();
+    __shared__ uint64_t f_lds[72 * 64];  // one wave per workgroup (TDEC kernels: __launch_bounds__(64))
+    uint64_t* f = f_lds + threadIdx.x;
+    lds_st_fp6(f, 0, fp6_one());
+    lds_st_fp6(f, 1, fp6_zero());
+    lds_fence();
 #pragma unroll 1
     for (int k = 0; k < kMillerSteps; ++k) {
 #pragma unroll 1
@@ -851,15 +917,15 @@ BD Fp12 miller_loop2(const uint32_t* c1, const Fp& a1, const Fp& b1, const Fp& z
                 const Fp a = j ? a2 : a1, b = j ? b2 : b1;
                 if constexpr (JAC) {
                     const Fp z = j ? z2 : z1;
-                    fp12_mul_by_014_v(f, fp2_mul_fp(c.c2, z), fp2_mul_fp(c.c1, a), fp2_mul_fp(c.c0, b));
+                    lds_mul_by_014(f, fp2_mul_fp(c.c2, z), fp2_mul_fp(c.c1, a), fp2_mul_fp(c.c0, b));
                 } else {
-                    ell(f, c, a, b);
+                    lds_mul_by_014(f, c.c2, fp2_mul_fp(c.c1, a), fp2_mul_fp(c.c0, b));
                 }
             }
         }
-        if ((kMillerSqr.w[k >> 5] >> (k & 31)) & 1u) f = fp12_sqr_v(f);
+        if ((kMillerSqr.w[k >> 5] >> (k & 31)) & 1u) lds_sqr(f);
     }
-    return fp12_conj(f);
+    return fp12_conj({lds_fp6(f, 0), lds_fp6(f, 1)});
 }
 
 // one pairing check: prod e(P_i, Q_i) == 1 over the two prepared pairs
