@@ -233,7 +233,7 @@ def fp_per_share(prof: dict, key: str, n_shares: int) -> float:
 # encrypt / decrypt_share kernels in the same profile are not part of it).
 TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_prepare", "tdec_ct_verify", "tdec_pair_index", "tdec_pk_table",
                        "tdec_iota", "tdec_group_marks", "tdec_batch_heads", "tdec_batch_desc", "tdec_batch_leaves",
-                       "tdec_batch_check", "tdec_verify_shares", "tdec_select", "tdec_combine_msm",
+                       "tdec_bin_root", "tdec_bin_step", "tdec_verify_shares", "tdec_select", "tdec_combine_msm",
                        "tdec_status_merge", "tdec_index_sanitize")
 
 
@@ -410,7 +410,7 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             "peak_source": "v_mad_u64_u32 4.44 cyc/wave-instr/SIMD (profiles/r01/valu_issue_rates_ubench2.txt) "
                            "x 1024 SIMDs x 64 lanes x 2.4 GHz",
             "note": "each Fp mul also issues 288 v_addc (carry) + ~95 other VALU: frac <= ~0.5 by construction",
-            "occupancy": kernel_meta(["tdec_batch_leaves", "tdec_batch_check", "tdec_verify_shares",
+            "occupancy": kernel_meta(["tdec_batch_leaves", "tdec_bin_step", "tdec_verify_shares",
                                       "tdec_ct_prepare", "tdec_ct_verify", "tdec_combine_msm"]),
         }
         floor = fp_count_floor()

@@ -27,7 +27,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 47;
+constexpr int kNumSlots = 50;
 
 struct Buf {
     void* p = nullptr;
@@ -737,8 +737,9 @@ int prepare_pks(hbg_ctx* c, uint32_t n_pk, const uint8_t* dpk, void** paff, void
 
 // Batched PublicKeyShare::verify_decryption_share (tdec_kernels.hip, "batched
 // share verification"): sort shares by ciphertext, cut batches of <= 64,
-// weighted batch sums, then four check rounds (batch, 16-group, quad, single
-// share).  Every round's work count is a device word read by the kernels
+// weighted batch sums, then the batch round and six binary rounds (check the
+// left child of every failing node, derive the right one in GT) and a
+// per-share round for capacity overflow.  Every round's work count is a device word read by the kernels
 // (grids sized for the bound): no host synchronisation (HBG_ASYNC contract).
 // A pk table costs ~2k G1 scalar multiplications to build and saves ~60 G1
 // doublings per share verified under that key.
@@ -786,20 +787,25 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     HBG_CHECK(scratch(c, 22, 64, &cnt));
     const uint32_t nb = bls::tdec_batch_bound(n, n_keys);
     bls::tdec_debug_bounds(n, nb, n_keys, (uint64_t)n_pk + 1);
-    void *sums, *lok, *items, *items2, *fails;
+    // the binary rounds' item lists and GT values (two of each, alternating):
+    // cap items per round — ~ one per bad share; a round's overflow goes to
+    // the per-share list, so memory stays bounded on any input
+    const uint32_t cap = nb > 64 ? nb : 64u;
+    void *sums, *lok, *items, *items2, *fails, *gt0, *gta, *gtb;
     HBG_CHECK(scratch(c, 23, (size_t)bls::kBatchSumBytes * nb, &sums));
     HBG_CHECK(scratch(c, 24, (size_t)bls::kBatchShares * nb, &lok));
-    HBG_CHECK(scratch(c, 25, (size_t)bls::kCheckItemBytes * 4 * nb, &items));
-    HBG_CHECK(scratch(c, 28, (size_t)bls::kCheckItemBytes * 16 * nb, &items2));
+    HBG_CHECK(scratch(c, 25, (size_t)bls::kBinItemBytes * cap, &items));
+    HBG_CHECK(scratch(c, 28, (size_t)bls::kBinItemBytes * cap, &items2));
     HBG_CHECK(scratch(c, 26, 4ull * n, &fails));
-    // counts: [0] 16-group items, [1] failing shares, [2] quad items, [3] batches
+    HBG_CHECK(scratch(c, 47, (size_t)bls::kGtBytes * 2 * nb, &gt0));
+    HBG_CHECK(scratch(c, 48, (size_t)bls::kGtBytes * 2 * cap, &gta));
+    HBG_CHECK(scratch(c, 49, (size_t)bls::kGtBytes * 2 * cap, &gtb));
+    // counts: [1] per-share list, [3] batches, [4 + r] items of binary round r + 1
     uint32_t* counts = (uint32_t*)cnt;
     const bls::BatchDesc* ds = (const bls::BatchDesc*)desc;
     const uint32_t *pm = (const uint32_t*)perm, *sm = (const uint32_t*)sums;
     const uint8_t* lk = (const uint8_t*)lok;
-    auto* it1 = (bls::CheckItem*)items;
-    auto* it2 = (bls::CheckItem*)items2;
-    HBG_TRY(hipMemsetAsync(counts, 0, 12, c->stream));
+    HBG_TRY(hipMemsetAsync(counts, 0, 4 * (5 + bls::kBinRounds), c->stream));
     HBG_TRY(bls::launch_tdec_batch_plan(n, n_keys, dsc, (uint32_t*)keys, (uint32_t*)perm, (uint32_t*)ta,
                                         (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, counts + 3, c->stream));
     HBG_DBG_STEP(c, "batch_plan");
@@ -845,20 +851,21 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
     if (after_leaves) HBG_CHECK(after_leaves());
-    // round 0: every batch sum; failing batches push their 16-share groups
-    HBG_TRY(bls::launch_tdec_batch_check(nb, counts + 3, nullptr, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it1,
-                                         counts, (uint32_t*)fails, counts + 1, c->stream));
-    HBG_DBG_STEP(c, "check round 0");
-    // round 1: 16-share groups; failing ones push their quads
-    HBG_TRY(bls::launch_tdec_batch_check(4 * nb, counts, it1, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, it2,
-                                         counts + 2, (uint32_t*)fails, counts + 1, c->stream));
-    HBG_DBG_STEP(c, "check round 1");
-    // round 2: quads; failing ones append their shares
-    HBG_TRY(bls::launch_tdec_batch_check(16 * nb, counts + 2, it2, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok,
-                                         nullptr, nullptr, (uint32_t*)fails, counts + 1, c->stream));
-    HBG_DBG_STEP(c, "check round 2");
-    // round 3: the shares of failing quads, one by one (the reference's equation
-    // on the points the leaves decoded)
+    // round 0: every batch sum; a failing batch's value and its left half go to round 1
+    auto list = [&](int r) { return (bls::BinItem*)((r & 1) ? items : items2); };  // round r's items (r >= 1)
+    auto gts = [&](int r) { return (uint32_t*)(r == 0 ? gt0 : ((r & 1) ? gta : gtb)); };  // written by round r
+    HBG_TRY(bls::launch_tdec_bin_root(nb, counts + 3, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, gts(0), list(1),
+                                      counts + 4, cap, (uint32_t*)fails, counts + 1, c->stream));
+    HBG_DBG_STEP(c, "binary round 0");
+    // rounds 1..6 (halves .. single shares): check the left child, derive the right
+    for (int r = 1; r <= bls::kBinRounds; ++r) {
+        HBG_TRY(bls::launch_tdec_bin_step(cap, counts + 3 + r, list(r), ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok,
+                                          gts(r - 1), gts(r), list(r + 1), counts + 4 + r, cap, (uint32_t*)fails,
+                                          counts + 1, c->stream));
+        HBG_DBG_STEP(c, "binary round");
+    }
+    // the shares of nodes past a round's capacity, one by one (the reference's
+    // equation on the points the leaves decoded; normally none)
     HBG_TRY(bls::launch_tdec_verify_shares(n, counts + 1, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW, paff,
                                            pst, dok, c->stream, (const uint32_t*)fails, share_aff));
     HBG_DBG_STEP(c, "per-share round");

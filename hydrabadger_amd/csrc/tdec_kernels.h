@@ -14,7 +14,10 @@ constexpr uint32_t kBatchShares = 64;             // batched verification: share
 
 struct BatchDesc;
 struct CheckItem;
-constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBatchSumBytes = 21 * 2 * 36 * 4;
+constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBinItemBytes = 16;
+constexpr uint32_t kBatchSumBytes = 64 * 2 * 36 * 4;  // per batch: the binary tree's root + left nodes (2 G1 sums each)
+constexpr uint32_t kGtBytes = 144 * 4;                // a GT value (Fp12)
+constexpr int kBinRounds = 6;                          // binary group-testing rounds after the batch check
 constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G2 Jacobian sums of 21 tree nodes
 // The sig_* check rounds run in launches of at most kResidentBlocks 64-lane
 // blocks (2 waves per SIMD x 1,024 SIMDs: the TDec kernels' resident limit);
@@ -58,11 +61,21 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     uint8_t* leaf_ok, hipStream_t st, uint32_t* share_aff = nullptr);
 size_t tdec_pk_table_bytes(uint32_t n_pk);
 hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st);
-hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const CheckItem* items,
-                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
-                                   const uint8_t* leaf_ok, const uint32_t* ct_u, const uint32_t* coefH,
-                                   const uint32_t* coefW, uint8_t* ok, CheckItem* next, uint32_t* next_n,
-                                   uint32_t* fail_list, uint32_t* fail_n, hipStream_t st);
+// Binary group testing (tdec_kernels.hip "batched share verification"):
+// round 0 over the batches, then kBinRounds rounds over BinItem lists (count:
+// a device word; items past next_cap hand their leaves to the per-share list).
+// gt_out / gt_in: 2 GT values per item of the writing / previous round.
+struct BinItem;
+hipError_t launch_tdec_bin_root(uint32_t cap, const uint32_t* nb_dev, const BatchDesc* desc, const uint32_t* perm,
+                                const uint32_t* sums, const uint8_t* leaf_ok, const uint32_t* ct_u,
+                                const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok, uint32_t* gt_out,
+                                BinItem* next, uint32_t* next_n, uint32_t next_cap, uint32_t* fail_list,
+                                uint32_t* fail_n, hipStream_t st);
+hipError_t launch_tdec_bin_step(uint32_t cap, const uint32_t* n_dev, const BinItem* items, const BatchDesc* desc,
+                                const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
+                                const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
+                                const uint32_t* gt_in, uint32_t* gt_out, BinItem* next, uint32_t* next_n,
+                                uint32_t next_cap, uint32_t* fail_list, uint32_t* fail_n, hipStream_t st);
 hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
                            const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st);
 hipError_t launch_wire_verify_frames(uint64_t n, const uint32_t* pk_aff, const int32_t* pk_status, uint32_t n_pk,

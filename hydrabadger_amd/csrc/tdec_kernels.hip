@@ -936,14 +936,14 @@ BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool us
     return fp12_is_one(f);
 }
 
-// e(P1, Q1) e(P2, Q2) == 1 for Jacobian P1, P2 (an identity point: its pair is skipped)
-BD bool pairing_check2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2, const G1& p2, bool use2) {
+// e(P1, Q1) e(P2, Q2) in GT for Jacobian P1, P2 (an identity point: its pair is skipped)
+BD Fp12 pairing_value2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2, const G1& p2, bool use2) {
     const bool u1 = !fp_is_zero(p1.z), u2 = use2 && !fp_is_zero(p2.z);
     const Fp z1 = fp_sqr(p1.z), z2 = fp_sqr(p2.z);
     Fp12 f = miller_loop2<true>(c1, fp_mul(p1.x, p1.z), p1.y, fp_mul(z1, p1.z), u1, c2, fp_mul(p2.x, p2.z), p2.y,
                                 fp_mul(z2, p2.z), u2);
     final_exponentiation(&f);
-    return fp12_is_one(f);
+    return f;
 }
 
 // ------------------------------------------------------------------ kernels
@@ -1079,13 +1079,21 @@ __global__ __launch_bounds__(256) void tdec_index_sanitize(uint64_t n, const uin
 // e(S_i, H) == e(PK_i, W) for all i in a batch  <=  e(sum r_i S_i, H) ==
 // e(sum r_i PK_i, W) with 64-bit weights r_i derived from a digest of the
 // whole batch (Bellare-Garay-Rabin small-exponent batch test; a batch holding
-// an invalid share passes with probability <= 2^-63).  A batch is up to 64 shares of one
-// ciphertext, tested as a 4-ary tree: round 0 checks every batch sum, a
-// failing batch checks its four 16-share groups (round 1), a failing group its
-// four quads (round 2), and the shares of a failing quad are checked one by
-// one with the plain per-share test (round 3, tdec_verify_shares) — so every
-// reported 0 comes from the reference's own per-share equation and every 1
-// from a passing (sub)group.
+// an invalid share passes with probability <= 2^-63).  A batch is up to 64
+// shares of one ciphertext, tested as a BINARY tree with sibling derivation
+// (round 5): round 0 checks every batch sum; a failing node's left child is
+// checked and its right child's value is DERIVED — the checks are values in
+// GT (e(sum r S, H) e(-sum r PK, W) after the final exponentiation), which
+// multiply over disjoint leaf sets, so right = parent * left^-1 (the inverse
+// in the cyclotomic subgroup is the conjugate).  Each failing node costs one
+// pairing, and six rounds (32, 16, 8, 4, 2, 1 shares) reach the single
+// shares.  A single's value is g^r for g = e(S, H) e(-PK, W) and its weight r
+// (a + b x^2 with a odd, < 2^161 < the group order: never 0 mod r), so it is
+// 1 exactly when the reference's per-share equation holds: every reported 0
+// is that equation's verdict, every 1 a passing (sub)tree's.  Round 4's 4-ary
+// tree (4 checks per failing node, three rounds) ran its rounds at 2-4 full
+// generations of one wave per SIMD; here a round holds ~one check per bad
+// share (<= 64 k items at 1 % of 6.4 M: one generation).
 struct BatchDesc {
     uint32_t start, end, ct, pad;
 };
@@ -1094,11 +1102,26 @@ struct CheckItem {
 };
 constexpr uint32_t kJacWords = 36;                    // Jacobian G1: x, y, z
 constexpr uint32_t kSumWords = 2 * kJacWords;         // (sum r S, sum r PK)
-// group-testing tree per batch of 64: nodes 0..15 = quads (4 shares), 16..19 =
-// 16-share groups, 20 = the batch.  At 1 % bad shares this costs ~7.8 pairing
-// checks per 64 shares (9.7 for a 64 -> 8 -> 1 tree, 64 for none).
+// 4-ary group-testing tree of the coin-share batches (sig_*): nodes 0..15 =
+// quads (4 shares), 16..19 = 16-share groups, 20 = the batch.
 constexpr uint32_t kNodes = 21, kNodeBatch = 20, kNode16 = 16;
-constexpr uint32_t kBatchSumWords = kNodes * kSumWords;
+// Binary tree of the decryption-share batches: heap ids (root 1, children 2h
+// and 2h + 1, single shares 64..127).  Stored per batch: the root (slot 0)
+// and every LEFT node h (slot h / 2) — the right ones are derived.
+constexpr uint32_t kBinSlots = 64;
+constexpr uint32_t kBatchSumWords = kBinSlots * kSumWords;
+static_assert(kBatchSumBytes == 4 * kBatchSumWords, "tdec_kernels.h");
+constexpr uint32_t kGtWords = 144;  // a GT value: Fp12 after the final exponentiation
+struct BinItem {
+    uint32_t b;      // batch
+    uint32_t h;      // the LEFT child to check (even heap id); its sibling h + 1 is derived
+    uint32_t ppos;   // the parent's GT value: item ppos of the previous round (round 1: batch ppos)
+    uint32_t pside;  // 0: that item's checked node, 1: its derived node
+};
+static_assert(sizeof(BinItem) == kBinItemBytes, "tdec_kernels.h");
+BD uint32_t bin_depth(uint32_t h) { return 31u - __builtin_clz(h); }
+BD uint32_t bin_size(uint32_t h) { return kBatchShares >> bin_depth(h); }
+BD uint32_t bin_first(uint32_t h) { return (h - (1u << bin_depth(h))) * bin_size(h); }
 
 __global__ void tdec_iota(uint32_t n, uint32_t* __restrict__ v) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1277,23 +1300,24 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
         }
     }
     leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
+    // the binary tree's left nodes (slot h / 2) and the root (slot 0): the
+    // weighted single of an even lane, then after each butterfly level the
+    // sum of every even group of 2m lanes, held by the group's first lane
     uint32_t* out = sums + (uint64_t)b * kBatchSumWords;
+    if ((lane & 1u) == 0) {
+        store_jac(out + (32u + (lane >> 1)) * kSumWords, A);
+        store_jac(out + (32u + (lane >> 1)) * kSumWords + kJacWords, B);
+    }
 #pragma unroll 1
-    for (int m = 1; m < 64; m <<= 1) {
+    for (uint32_t m = 1; m < 64; m <<= 1) {
         A = g1_add(A, g1_shfl_xor(A, m));
         B = g1_add(B, g1_shfl_xor(B, m));
-        if (m == 2 && (lane & 3u) == 0) {  // quad sums (nodes 0..15)
-            store_jac(out + (lane >> 2) * kSumWords, A);
-            store_jac(out + (lane >> 2) * kSumWords + kJacWords, B);
+        const uint32_t gsz = 2u * m;  // group size; group j = lane / gsz is heap node 64 / gsz + j
+        const uint32_t slot = gsz == 64 ? 0u : (64u / gsz + lane / gsz) / 2u;
+        if ((lane & (2u * gsz - 1u)) == 0 || (gsz == 64 && lane == 0)) {
+            store_jac(out + slot * kSumWords, A);
+            store_jac(out + slot * kSumWords + kJacWords, B);
         }
-        if (m == 8 && (lane & 15u) == 0) {  // 16-share group sums (nodes 16..19)
-            store_jac(out + (kNode16 + (lane >> 4)) * kSumWords, A);
-            store_jac(out + (kNode16 + (lane >> 4)) * kSumWords + kJacWords, B);
-        }
-    }
-    if (lane == 0) {
-        store_jac(out + kNodeBatch * kSumWords, A);
-        store_jac(out + kNodeBatch * kSumWords + kJacWords, B);
     }
 }
 
@@ -1336,42 +1360,125 @@ BD void batch_tree_step(bool pass, const CheckItem& it, const BatchDesc& d, cons
     }
 }
 
-// One lane per check item: e(sum r S, H) * e(-sum r PK, W) == 1.  Items:
-// the list `items` (count *n_dev) or, with items == null, every batch
-// (count *n_dev = the batch count); the grid covers `cap` items, lanes past
-// the device count return at once.
-TDEC_WAVE1_KERNEL void tdec_batch_check(uint32_t cap, const uint32_t* __restrict__ n_dev, const CheckItem* __restrict__ items,
-                                                       const BatchDesc* __restrict__ desc,
-                                                       const uint32_t* __restrict__ perm,
-                                                       const uint32_t* __restrict__ sums,
-                                                       const uint8_t* __restrict__ leaf_ok,
-                                                       const uint32_t* __restrict__ ct_u,
-                                                       const uint32_t* __restrict__ coefH,
-                                                       const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok,
-                                                       CheckItem* __restrict__ next, uint32_t* __restrict__ next_n,
-                                                       uint32_t* __restrict__ fail_list,
-                                                       uint32_t* __restrict__ fail_n) {
-    const uint64_t i = grid_lane();
-    if (i >= dev_count(n_dev, cap)) return;
-    const CheckItem it = items ? items[i] : CheckItem{(uint32_t)i, kNodeBatch};
-#ifdef HBG_DEBUG_CHECKS
-    if (!HBG_DBG_RANGE(it.b, g_dbg[1], "check it.b") || !HBG_DBG_RANGE(it.node, kNodes, "check node")) return;
-#endif
-    const BatchDesc d = desc[it.b];
-#ifdef HBG_DEBUG_CHECKS
-    if (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "check d.end") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "check d.ct")) return;
-#endif
-    const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
-    const uint32_t l0 = node_first(it.node);
-    if (!node_any_valid(lok, l0, l0 + node_size(it.node))) return;  // nothing valid to vouch for: those shares stay 0
-    const uint32_t* sm = sums + (uint64_t)it.b * kBatchSumWords + it.node * kSumWords;
+// GT values of the binary rounds (kGtWords words, the Fp12's 12 Fp in order)
+BD void store_gt(uint32_t* d, const Fp12& v) {
+    const Fp x[12] = {v.c0.c0.c0, v.c0.c0.c1, v.c0.c1.c0, v.c0.c1.c1, v.c0.c2.c0, v.c0.c2.c1,
+                      v.c1.c0.c0, v.c1.c0.c1, v.c1.c1.c0, v.c1.c1.c1, v.c1.c2.c0, v.c1.c2.c1};
+#pragma unroll
+    for (int i = 0; i < 12; ++i) store_fp(d + 12 * i, x[i]);
+}
+BD Fp12 load_gt(const uint32_t* d) {
+    auto f2 = [&](int i) { return Fp2{load_fp(d + 12 * i), load_fp(d + 12 * i + 12)}; };
+    return {{f2(0), f2(2), f2(4)}, {f2(6), f2(8), f2(10)}};
+}
+
+// GT value of one stored node (slot) of batch d: e(sum r S, H) e(-sum r PK, W)
+BD Fp12 bin_node_value(const uint32_t* __restrict__ sums, uint32_t b, uint32_t slot, const BatchDesc& d,
+                       const uint32_t* __restrict__ ct_u, const uint32_t* __restrict__ coefH,
+                       const uint32_t* __restrict__ coefW) {
+    const uint32_t* sm = sums + (uint64_t)b * kBatchSumWords + slot * kSumWords;
     const G1 a = load_jac(sm), bj = load_jac(sm + kJacWords);
     const bool w_inf = ct_u[32ull * d.ct + 25] != 0;
-    // e(sum r S, H) e(-sum r PK, W) == 1, on the Jacobian sums directly
-    const bool pass = pairing_check2_jac(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a,
-                                         coefW + (uint64_t)d.ct * kLineWordsPerPoint, {bj.x, fp_neg(bj.y), bj.z},
-                                         !w_inf);
-    batch_tree_step(pass, it, d, lok, perm, ok, next, next_n, fail_list, fail_n);
+    return pairing_value2_jac(coefH + (uint64_t)d.ct * kLineWordsPerPoint, a, coefW + (uint64_t)d.ct * kLineWordsPerPoint,
+                              {bj.x, fp_neg(bj.y), bj.z}, !w_inf);
+}
+
+// One tree node's verdict: a pass vouches for its valid leaves; a failing
+// single is an invalid share (its ok byte stays 0); a failing larger node is
+// pushed as the next round's item (its left child to check, its own value
+// stored at this item's side slot for the derivation) — or, past the next
+// round's capacity, its valid leaves go to the per-share round.
+BD void bin_node_verdict(uint32_t h, bool pass, const Fp12& v, uint32_t b, const BatchDesc& d, const uint8_t* lok,
+                         const uint32_t* __restrict__ perm, uint8_t* __restrict__ ok, uint32_t pos, uint32_t side,
+                         uint32_t* __restrict__ gt_out, BinItem* __restrict__ next, uint32_t* __restrict__ next_n,
+                         uint32_t next_cap, uint32_t* __restrict__ fail_list, uint32_t* __restrict__ fail_n) {
+    const uint32_t l0 = bin_first(h), l1 = l0 + bin_size(h);
+    if (pass) {
+        for (uint32_t l = l0; l < l1; ++l)
+            if (lok[l]) ok[perm[d.start + l]] = 1;
+        return;
+    }
+    if (l1 - l0 == 1) return;
+    const uint32_t q = atomicAdd(next_n, 1u);
+    if (q < next_cap) {
+        store_gt(gt_out + (uint64_t)(2 * pos + side) * kGtWords, v);
+        next[q] = BinItem{b, 2 * h, pos, side};
+    } else {
+        for (uint32_t l = l0; l < l1; ++l)
+            if (lok[l]) fail_list[atomicAdd(fail_n, 1u)] = perm[d.start + l];
+    }
+}
+
+// Round 0, one lane per batch: the batch sum (slot 0).  A failing batch's
+// value goes to gt_out[2 b] and its left half to the round-1 list.
+TDEC_WAVE1_KERNEL void tdec_bin_root(uint32_t cap, const uint32_t* __restrict__ nb_dev,
+                                     const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
+                                     const uint32_t* __restrict__ sums, const uint8_t* __restrict__ leaf_ok,
+                                     const uint32_t* __restrict__ ct_u, const uint32_t* __restrict__ coefH,
+                                     const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok,
+                                     uint32_t* __restrict__ gt_out, BinItem* __restrict__ next,
+                                     uint32_t* __restrict__ next_n, uint32_t next_cap,
+                                     uint32_t* __restrict__ fail_list, uint32_t* __restrict__ fail_n) {
+    const uint64_t i = grid_lane();
+    if (i >= dev_count(nb_dev, cap)) return;
+    const uint32_t b = (uint32_t)i;
+    const BatchDesc d = desc[b];
+#ifdef HBG_DEBUG_CHECKS
+    if (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "root d.end") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "root d.ct")) return;
+#endif
+    const uint8_t* lok = leaf_ok + (uint64_t)b * kBatchShares;
+    if (!node_any_valid(lok, 0, kBatchShares)) return;  // nothing valid to vouch for: those shares stay 0
+    const Fp12 v = bin_node_value(sums, b, 0, d, ct_u, coefH, coefW);
+    bin_node_verdict(1, fp12_is_one(v), v, b, d, lok, perm, ok, b, 0, gt_out, next, next_n, next_cap, fail_list,
+                     fail_n);
+}
+
+// Rounds 1..6, one lane per item (a failing parent): check its left child,
+// derive the right one (parent * conj(left): the GT values multiply over the
+// disjoint halves; a side without valid leaves is the identity, so the other
+// side equals the parent and needs no check either), verdict for both.
+TDEC_WAVE1_KERNEL void tdec_bin_step(uint32_t cap, const uint32_t* __restrict__ n_dev,
+                                     const BinItem* __restrict__ items, const BatchDesc* __restrict__ desc,
+                                     const uint32_t* __restrict__ perm, const uint32_t* __restrict__ sums,
+                                     const uint8_t* __restrict__ leaf_ok, const uint32_t* __restrict__ ct_u,
+                                     const uint32_t* __restrict__ coefH, const uint32_t* __restrict__ coefW,
+                                     uint8_t* __restrict__ ok, const uint32_t* __restrict__ gt_in,
+                                     uint32_t* __restrict__ gt_out, BinItem* __restrict__ next,
+                                     uint32_t* __restrict__ next_n, uint32_t next_cap,
+                                     uint32_t* __restrict__ fail_list, uint32_t* __restrict__ fail_n) {
+    const uint64_t i = grid_lane();
+    if (i >= dev_count(n_dev, cap)) return;
+    const BinItem it = items[i];
+#ifdef HBG_DEBUG_CHECKS
+    if (!HBG_DBG_RANGE(it.b, g_dbg[1], "step it.b") || !HBG_DBG_RANGE(it.h, 128, "step h")) return;
+#endif
+    const BatchDesc d = desc[it.b];
+    const uint8_t* lok = leaf_ok + (uint64_t)it.b * kBatchShares;
+    const uint32_t hl = it.h, s = bin_size(hl), l0 = bin_first(hl);
+    const bool lany = node_any_valid(lok, l0, l0 + s), rany = node_any_valid(lok, l0 + s, l0 + 2 * s);
+    Fp12 lv = fp12_one();
+    bool lpass = true;
+    if (lany && rany) {
+        lv = bin_node_value(sums, it.b, hl / 2, d, ct_u, coefH, coefW);
+        lpass = fp12_is_one(lv);
+    }
+    const Fp12 pv = load_gt(gt_in + (uint64_t)(2 * it.ppos + it.pside) * kGtWords);  // != 1: the parent failed
+    Fp12 rv = pv;
+    bool rpass = !rany;
+    if (lany && !rany) {
+        lv = pv;
+        lpass = false;
+    } else if (lany && !lpass) {
+        const Fp12 cl = fp12_conj(lv);
+        fp12_mul_n(&rv, &pv, &cl);
+        rpass = fp12_is_one(rv);
+    }
+    if (lany)
+        bin_node_verdict(hl, lpass, lv, it.b, d, lok, perm, ok, (uint32_t)i, 0, gt_out, next, next_n, next_cap,
+                         fail_list, fail_n);
+    if (rany)
+        bin_node_verdict(hl + 1, rpass, rv, it.b, d, lok, perm, ok, (uint32_t)i, 1, gt_out, next, next_n, next_cap,
+                         fail_list, fail_n);
 }
 
 TDEC_WAVE1_KERNEL void tdec_ct_verify(uint32_t n, const uint32_t* __restrict__ ct_u,
@@ -2844,15 +2951,27 @@ hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t*
     return hipGetLastError();
 }
 
-hipError_t launch_tdec_batch_check(uint32_t cap, const uint32_t* n_dev, const CheckItem* items,
-                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
-                                   const uint8_t* leaf_ok, const uint32_t* ct_u, const uint32_t* coefH,
-                                   const uint32_t* coefW, uint8_t* ok, CheckItem* next, uint32_t* next_n,
-                                   uint32_t* fail_list, uint32_t* fail_n, hipStream_t st) {
-    HBG_COUNT_MARK("tdec_batch_check", st);
+hipError_t launch_tdec_bin_root(uint32_t cap, const uint32_t* nb_dev, const BatchDesc* desc, const uint32_t* perm,
+                                const uint32_t* sums, const uint8_t* leaf_ok, const uint32_t* ct_u,
+                                const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok, uint32_t* gt_out,
+                                BinItem* next, uint32_t* next_n, uint32_t next_cap, uint32_t* fail_list,
+                                uint32_t* fail_n, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_bin_root", st);
     if (cap == 0) return hipSuccess;
-    tdec_batch_check<<<item_grid(cap), dim3(64), 0, st>>>(cap, n_dev, items, desc, perm, sums, leaf_ok, ct_u,
-                                                              coefH, coefW, ok, next, next_n, fail_list, fail_n);
+    tdec_bin_root<<<item_grid(cap), dim3(64), 0, st>>>(cap, nb_dev, desc, perm, sums, leaf_ok, ct_u, coefH, coefW, ok,
+                                                       gt_out, next, next_n, next_cap, fail_list, fail_n);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_bin_step(uint32_t cap, const uint32_t* n_dev, const BinItem* items, const BatchDesc* desc,
+                                const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
+                                const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
+                                const uint32_t* gt_in, uint32_t* gt_out, BinItem* next, uint32_t* next_n,
+                                uint32_t next_cap, uint32_t* fail_list, uint32_t* fail_n, hipStream_t st) {
+    HBG_COUNT_MARK("tdec_bin_step", st);
+    if (cap == 0) return hipSuccess;
+    tdec_bin_step<<<item_grid(cap), dim3(64), 0, st>>>(cap, n_dev, items, desc, perm, sums, leaf_ok, ct_u, coefH,
+                                                       coefW, ok, gt_in, gt_out, next, next_n, next_cap, fail_list,
+                                                       fail_n);
     return hipGetLastError();
 }
 hipError_t launch_tdec_select(uint32_t n_ct, uint32_t N, uint32_t t, const uint8_t* ct_ok, const uint8_t* ok,

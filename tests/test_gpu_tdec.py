@@ -250,7 +250,7 @@ def test_golden_tdec_on_gpu():
     assert [p.hex() for p in pts] == [c["plaintext"] for c in sc["cts"]]
 
 
-@pytest.mark.parametrize("bad_rate,seed", [(0.0, 1), (0.03, 2), (0.3, 3)])
+@pytest.mark.parametrize("bad_rate,seed", [(0.0, 1), (0.03, 2), (0.3, 3), (1.0, 4)])
 def test_batched_verify_equals_per_share(bad_rate, seed):
     """hbg_tdec_verify_shares' batched schedule (weighted batch sums per
     ciphertext, sub-batches of 8, per-share fallback) returns exactly the bits
