@@ -240,33 +240,35 @@ TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_prepare", "tdec_ct_verify", "
 def tdec_pmc_traffic(n_shares: int) -> dict:
     """HBM bytes of one ThresholdDecrypt call at the bench shape (100k x 64,
     1 % bad), from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE per kernel, profiles/r04/pmc_tdec_100k.json: the register-
-    resident tower of round 4); most of it is still scratch (the final
-    exponentiation's parked Fp12 values, the G2 steps' call frames), since a
-    share is 48 B."""
-    path = os.path.join(ROOT, "profiles", "r04", "pmc_tdec_100k.json")
+    WRITE_SIZE per dispatch, profiles/r05/pmc_tdec_100k.json over
+    tools/tdec_kbench.py --cts 100000: the LDS Miller accumulator and the
+    binary check rounds); per-dispatch averages times the dispatches per call."""
+    path = os.path.join(ROOT, "profiles", "r05", "pmc_tdec_100k.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return {}
+    per_call = {"tdec_bin_step": 6}
     per_kernel = {}
     for name, v in d.items():
         short = name.split("::")[-1].split("<")[0]
-        if short in TDEC_DRIVER_KERNELS and isinstance(v, dict) and "hbm_read_bytes_corrected" in v:
-            per_kernel[short] = v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
+        if "bls_lat" in name or short not in TDEC_DRIVER_KERNELS or not isinstance(v, dict):
+            continue
+        if "hbm_read_bytes_corrected" in v:
+            per_kernel[short] = (v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]) * per_call.get(short, 1)
     if not per_kernel or n_shares != 6_400_000:
         return {}
     total = sum(per_kernel.values())
     return {"bytes_per_call": total, "bytes_per_share": total / n_shares,
             "per_kernel_bytes_per_share": {k: v / n_shares for k, v in sorted(per_kernel.items(), key=lambda x: -x[1])},
-            "source": os.path.relpath(path, ROOT) + " (tools/gpu_r03c.sh via tools/gpu_r04z.sh at the round-4 head: rocprofv3 --pmc "
-                      "FETCH_SIZE / WRITE_SIZE passes over tools/tdec_kbench.py --cts 100000)"}
+            "source": os.path.relpath(path, ROOT) + " (tools/pmc_tdec.sh, KB_ARGS='--cts 100000 --reps 1', "
+                      "EXTRA_GROUPS='FETCH_SIZE WRITE_SIZE')"}
 
 
 def fp_count_floor() -> dict:
     """The batched verifier's executed Fp count with no bad share (no group
-    testing, no per-share fallback): profiles/r04/fpcount_batched_0pct.json."""
-    path = os.path.join(ROOT, "profiles", "r04", "fpcount_batched_0pct.json")
+    testing, no per-share fallback): profiles/r05/fpcount_batched_0pct.json."""
+    path = os.path.join(ROOT, "profiles", "r05", "fpcount_batched_0pct.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -283,6 +285,8 @@ def kernel_meta(names) -> dict:
         return {}
     out = {}
     for mangled, v in k.items():
+        if "bls_lat" in mangled:  # the one-wave latency build of the same kernels
+            continue
         for n in names:
             if f"{len(n)}{n}E" in mangled or f"{len(n)}{n}I" in mangled:
                 out[n] = {x: v[x] for x in ("vgpr", "agpr", "sgpr", "scratch_bytes", "lds_bytes",
