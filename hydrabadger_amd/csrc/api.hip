@@ -27,7 +27,7 @@ using namespace hbg;
 
 namespace {
 
-constexpr int kNumSlots = 50;
+constexpr int kNumSlots = 51;
 
 struct Buf {
     void* p = nullptr;
@@ -66,6 +66,7 @@ struct hbg_ctx {
     // a second stream for independent launches inside one call (fork / join by events)
     hipStream_t aux = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipEvent_t lines_ev = nullptr;  // stage_ct: the ciphertext line tables are built (aux stream)
     bool aux_open = false;  // forked and not yet joined (AuxJoin closes it on every return path)
     std::mutex mu;
 };
@@ -374,6 +375,7 @@ void hbg_free(hbg_ctx* c) {
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+    if (c->lines_ev) (void)hipEventDestroy(c->lines_ev);
     (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -412,9 +414,9 @@ static int join_aux(hbg_ctx* c) {
 // fork and join) still orders its stream after the aux work, so the next call
 // cannot reuse scratch the aux stream is still writing.
 struct AuxJoin {
-    hbg_ctx* c;
+    hbg_ctx* c;  // null: nothing to guard
     ~AuxJoin() {
-        if (c->aux_open) (void)join_aux(c);
+        if (c && c->aux_open) (void)join_aux(c);
     }
 };
 
@@ -680,7 +682,8 @@ struct CtTable {
 
 // Stage (host mode) and prepare a ciphertext table on the device.
 int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
-             const uint8_t* W96, uint32_t flags, CtTable& t, const uint8_t** dV, const uint64_t** dVoff) {
+             const uint8_t* W96, uint32_t flags, CtTable& t, const uint8_t** dV, const uint64_t** dVoff,
+             bool defer_lines = false) {
     const uint8_t *dU = U48, *dW = W96;
     *dV = V;
     *dVoff = V_off;
@@ -711,17 +714,27 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     t.coefH = (uint32_t*)ph;
     t.coefW = (uint32_t*)pwc;
     HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
-    void *pdg, *pws;
+    void *pdg, *pwa;
     HBG_CHECK(scratch(c, 40, 32ull * n_ct, &pdg));
-    HBG_CHECK(scratch(c, 44, 4ull * n_ct, &pws));
-    // W's half (decode + lines) on the aux stream, beside SHA3(V) + hash_g1_g2 + H's lines
-    AuxJoin guard{c};
+    HBG_CHECK(scratch(c, 50, (size_t)bls::kWAffBytes * n_ct, &pwa));
+    // U, W decode (the status the share leaves read) here; H = hash_g1_g2(U, V)
+    // and both line tables on the aux stream, which the caller joins (or, with
+    // defer_lines, waits for through wait_lines before the first pairing, so
+    // the tables build beside the share leaves)
+    HBG_TRY(bls::launch_tdec_ct_decode(n_ct, dU, dW, t.ct_u, t.ct_status, (uint32_t*)pwa, c->stream));
     HBG_CHECK(fork_aux(c));
-    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, (int32_t*)pws, t.coefW, c->aux));
-    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, dW, t.ct_u, t.ct_status, t.coefH, t.coefW,
-                                        (uint8_t*)pdg, c->stream));
-    HBG_CHECK(join_aux(c));
-    HBG_TRY(bls::launch_tdec_status_or(n_ct, t.ct_status, (const int32_t*)pws, c->stream));
+    AuxJoin guard{defer_lines ? nullptr : c};  // deferred: the caller's guard joins
+    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, (const uint32_t*)pwa, t.ct_u, t.ct_status, t.coefW, c->aux));
+    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, t.ct_status, t.coefH, (uint8_t*)pdg, c->aux));
+    if (!c->lines_ev) HBG_TRY(hipEventCreateWithFlags(&c->lines_ev, hipEventDisableTiming));
+    HBG_TRY(hipEventRecord(c->lines_ev, c->aux));
+    if (!defer_lines) HBG_CHECK(join_aux(c));
+    return HBG_OK;
+}
+
+// The stream waits for stage_ct's line tables (not for later aux work).
+int wait_lines(hbg_ctx* c) {
+    HBG_TRY(hipStreamWaitEvent(c->stream, c->lines_ev, 0));
     return HBG_OK;
 }
 
@@ -851,6 +864,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
     if (after_leaves) HBG_CHECK(after_leaves());
+    HBG_CHECK(wait_lines(c));  // H's and W's line tables (stage_ct, built beside the leaves)
     // round 0: every batch sum; a failing batch's value and its left half go to round 1
     auto list = [&](int r) { return (bls::BinItem*)((r & 1) ? items : items2); };  // round r's items (r >= 1)
     auto gts = [&](int r) { return (uint32_t*)(r == 0 ? gt0 : ((r & 1) ? gta : gtb)); };  // written by round r
@@ -896,7 +910,9 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     CtTable t;
     const uint8_t* dV;
     const uint64_t* dVoff;
-    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, t, &dV, &dVoff));
+    AuxJoin guard{c};
+    const bool batched = use_batched(c, n);
+    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, t, &dV, &dVoff, batched));
     HBG_DBG_STEP(c, "ct_prepare");
     const uint8_t *dpk = pk48, *dsh = share48;
     const uint32_t *dsc = share_ct, *dsp = share_pk;
@@ -931,9 +947,10 @@ int hbg_tdec_verify_shares(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const 
     void *paff, *pst;
     HBG_CHECK(prepare_pks(c, n_pk, dpk, &paff, &pst));
     HBG_DBG_STEP(c, "pk_prepare");
-    if (use_batched(c, n)) {
+    if (batched) {
         HBG_CHECK(verify_shares_batched(c, n_ct, t, t.U48, (uint32_t)n, n_pk, dsh, dsc, dsp, (const uint32_t*)paff,
                                         (const int32_t*)pst, dok));
+        HBG_CHECK(join_aux(c));
     } else {
         HBG_TRY(bls::launch_tdec_verify_shares(n, nullptr, dsh, dsc, dsp, t.ct_u, t.ct_status, t.coefH, t.coefW,
                                                (uint32_t*)paff, (int32_t*)pst, dok, c->stream));
@@ -1064,7 +1081,9 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     CtTable tab;
     const uint8_t* dV;
     const uint64_t* dVoff;
-    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, tab, &dV, &dVoff));
+    AuxJoin guard{c};
+    const bool batched = use_batched(c, n);
+    HBG_CHECK(stage_ct(c, n_ct, U48, V, V_off, W96, flags, tab, &dV, &dVoff, batched));
     const uint64_t vlen = (flags & HBG_DEVICE) ? 0 : V_off[n_ct];
     if (!(flags & HBG_DEVICE) && vlen && !plaintext) return HBG_E_ARG;
     const void *dpk, *dsh, *darr = nullptr;
@@ -1084,14 +1103,12 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     // drains, while next to the check rounds it takes their idle slots.
     void *ctok, *pairs, *okb, *sel;
     HBG_CHECK(scratch(c, 30, n_ct, &ctok));
-    AuxJoin guard{c};
     auto ct_verify = [&]() -> int {
         HBG_CHECK(fork_aux(c));
         HBG_TRY(bls::launch_tdec_ct_verify(n_ct, tab.ct_u, tab.ct_status, tab.coefH, tab.coefW, (uint8_t*)ctok,
                                            c->aux));
         return HBG_OK;
     };
-    const bool batched = use_batched(c, n);
     if (!batched) HBG_CHECK(ct_verify());
     // verify_decryption_share of every (ct, sender) share, batched
     HBG_CHECK(scratch(c, 15, 8ull * n, &pairs));

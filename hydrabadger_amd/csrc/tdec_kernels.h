@@ -24,13 +24,16 @@ constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G
 // their per-lane scratch (G2Prepared lines) is sized for kResidentBlocks * 64.
 constexpr uint32_t kResidentBlocks = 2048;
 
-// vdig: [n][32] scratch for SHA3(V) of the items with |V| > 64 (tdec_v_digest)
-hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
-                                    uint32_t* coefW, hipStream_t st);
-hipError_t launch_tdec_status_or(uint32_t n, int32_t* status, const int32_t* other, hipStream_t st);
+// Ciphertext table: tdec_ct_decode (U, W + subgroup checks -> ct_u, ct_status,
+// w_aff [n][kWAffBytes / 4]), then H's and W's G2Prepared lines (ct_prepare:
+// vdig [n][32] scratch for SHA3(V) of the items with |V| > 64; ct_prepare_w).
+constexpr uint32_t kWAffBytes = 48 * 4;
+hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, const uint8_t* W96, uint32_t* ct_u,
+                                 int32_t* ct_status, uint32_t* w_aff, hipStream_t st);
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
-                                  const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
-                                  uint32_t* coefW, uint8_t* vdig, hipStream_t st);
+                                  const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st);
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint32_t* w_aff, const uint32_t* ct_u,
+                                    const int32_t* ct_status, uint32_t* coefW, hipStream_t st);
 // xor_with_hash's keystream: out = in ^ keystream(seeds[k]) per item (status[k] != 0: skipped; nullable)
 hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uint8_t* in, const uint64_t* off,
                                      uint8_t* out, const int32_t* status, hipStream_t st);

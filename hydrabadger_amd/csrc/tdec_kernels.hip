@@ -3,9 +3,11 @@
 // Restates threshold_crypto [EXT] as hbbft's ThresholdDecrypt drives it
 // (reached from /root/reference/src/hydrabadger/
 // state.rs:486-487):
-//   tdec_ct_prepare     per ciphertext: decompress + subgroup-check U (G1) and
-//                       W (G2), H = hash_g1_g2(U, V) (SHA3 -> ChaChaRng ->
-//                       try-and-increment -> cofactor), G2Prepared lines of H, W
+//   tdec_ct_decode      per ciphertext: decompress + subgroup-check U (G1) and
+//                       W (G2) -> the ciphertext's status (what the leaves need)
+//   tdec_ct_prepare(_w) H = hash_g1_g2(U, V) (SHA3 -> ChaChaRng -> try-and-
+//                       increment -> cofactor), G2Prepared lines of H and W
+//                       (second stream, overlapped with the share leaves)
 //   tdec_pk_prepare     PublicKeyShare table: decompress + subgroup check
 //   tdec_verify_shares  PublicKeyShare::verify_decryption_share for every share:
 //                       e(S_i, H) * e(-PK_i, W) == 1 (one 2-pair Miller loop +
@@ -114,14 +116,18 @@ BD void sha3_bytes(const uint8_t* p, uint32_t len, uint8_t out[32]) {
 
 // ------------------------------------------------------------------ ChaCha20 (rand_chacha layout)
 BD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+// the byte rotations as one full-rate v_perm_b32 (v_alignbit, the compiler's
+// rotate, issues at half rate on gfx950)
+BD uint32_t rotl16p(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x01000302u); }
+BD uint32_t rotl8p(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x02010003u); }
 
 #define QR(a, b, c, d)            \
     a += b;                       \
-    d = rotl32(d ^ a, 16);        \
+    d = rotl16p(d ^ a);           \
     c += d;                       \
     b = rotl32(b ^ c, 12);        \
     a += b;                       \
-    d = rotl32(d ^ a, 8);         \
+    d = rotl8p(d ^ a);            \
     c += d;                       \
     b = rotl32(b ^ c, 7);
 
@@ -947,25 +953,42 @@ BD Fp12 pairing_value2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2,
 }
 
 // ------------------------------------------------------------------ kernels
-TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48,
-                                                      const uint8_t* __restrict__ V,
-                                                      const uint64_t* __restrict__ V_off,
-                                                      const uint8_t* __restrict__ vdig,
-                                                      const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
-                                                      int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH,
-                                                      uint32_t* __restrict__ coefW) {
+// Ciphertext preparation in two halves (round 5): tdec_ct_decode — U and W
+// decoded with their subgroup checks: the ciphertext's status, U's affine
+// record and W's affine point, all that the share leaves need — then, on the
+// second stream and overlapped with the leaves, the expensive half: H =
+// hash_g1_g2(U, V) (SHA3(V) for |V| > 64, try-and-increment, cofactor
+// clearing) and both G2Prepared line tables (tdec_ct_prepare, _w), which only
+// the check rounds and Ciphertext::verify read.
+constexpr uint32_t kWAffWords = 48;  // W affine: x.c0 x.c1 y.c0 y.c1
+TDEC_WAVE1_KERNEL void tdec_ct_decode(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ W96,
+                                      uint32_t* __restrict__ ct_u, int32_t* __restrict__ ct_status,
+                                      uint32_t* __restrict__ w_aff) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
-    int32_t st = 0;
     G1A u;
     G2A w;
-    if (!g1_decompress(U48 + 48ull * k, u, true)) st = HBG_E_INVALID_POINT;
+    const bool u_ok = g1_decompress(U48 + 48ull * k, u, true);
+    const bool w_ok = g2_decompress(W96 + 96ull * k, w, true);
     uint32_t* cu = ct_u + 32ull * k;
     store_fp(cu, u.x);
     store_fp(cu + 12, u.y);
     cu[24] = u.inf ? 1u : 0u;
-    ct_status[k] = st;  // W's verdict is or-ed in by tdec_status_or after tdec_ct_prepare_w
-    if (st != 0) return;
+    cu[25] = w.inf ? 1u : 0u;
+    uint32_t* wa = w_aff + (uint64_t)kWAffWords * k;
+    store_fp(wa, w.x.c0);
+    store_fp(wa + 12, w.x.c1);
+    store_fp(wa + 24, w.y.c0);
+    store_fp(wa + 36, w.y.c1);
+    ct_status[k] = u_ok && w_ok ? 0 : HBG_E_INVALID_POINT;
+}
+
+// H = hash_g1_g2(U, V) and its G2Prepared lines, for the decodable ciphertexts
+TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ V,
+                                       const uint64_t* __restrict__ V_off, const uint8_t* __restrict__ vdig,
+                                       const int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || ct_status[k] != 0) return;
     // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
     const uint64_t off = V_off[k], len = V_off[k + 1] - off;
     uint8_t m[64 + 48];
@@ -976,24 +999,15 @@ TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U
     g2_prepare(h.x, h.y, coefH + (uint64_t)k * 72 * kMillerSteps);
 }
 
-// The W half of ciphertext preparation (decode + subgroup check + the
-// G2Prepared lines of W): independent of V, so it runs on a second stream
-// while SHA3(V) and hash_g1_g2 run (stage_ct in api.hip).
-TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
-                                   int32_t* __restrict__ w_status, uint32_t* __restrict__ coefW) {
+// W's G2Prepared lines (W decoded by tdec_ct_decode)
+TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint32_t* __restrict__ w_aff,
+                                         const uint32_t* __restrict__ ct_u, const int32_t* __restrict__ ct_status,
+                                         uint32_t* __restrict__ coefW) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    G2A w;
-    const bool ok = g2_decompress(W96 + 96ull * k, w, true);
-    ct_u[32ull * k + 25] = w.inf ? 1u : 0u;
-    w_status[k] = ok ? 0 : HBG_E_INVALID_POINT;
-    if (ok && !w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
-}
-
-__global__ __launch_bounds__(256) void tdec_status_or(uint32_t n, int32_t* __restrict__ status,
-                                                      const int32_t* __restrict__ other) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n && status[k] == 0) status[k] = other[k];
+    if (k >= n || ct_status[k] != 0 || ct_u[32ull * k + 25] != 0) return;
+    const uint32_t* wa = w_aff + (uint64_t)kWAffWords * k;
+    g2_prepare({load_fp(wa), load_fp(wa + 12)}, {load_fp(wa + 24), load_fp(wa + 36)},
+               coefW + (uint64_t)k * 72 * kMillerSteps);
 }
 
 // Affine record (kAffWords words: x[12] y[12] inf): pk tables and the
@@ -2696,11 +2710,12 @@ TDEC_WAVE1_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict_
 #else
 }  // namespace bls
 namespace bls_lat {
+hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, const uint8_t* W96, uint32_t* ct_u,
+                                 int32_t* ct_status, uint32_t* w_aff, hipStream_t st);
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
-                                  const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
-                                  uint32_t* coefW, uint8_t* vdig, hipStream_t st);
-hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
-                                    uint32_t* coefW, hipStream_t st);
+                                  const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st);
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint32_t* w_aff, const uint32_t* ct_u,
+                                    const int32_t* ct_status, uint32_t* coefW, hipStream_t st);
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st);
 hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
@@ -2814,28 +2829,29 @@ hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uin
                                                                                              out, status);
     return hipGetLastError();
 }
+hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, const uint8_t* W96, uint32_t* ct_u,
+                                 int32_t* ct_status, uint32_t* w_aff, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_decode(n, U48, W96, ct_u, ct_status, w_aff, st));
+    HBG_COUNT_MARK("tdec_ct_decode", st);
+    if (n == 0) return hipSuccess;
+    tdec_ct_decode<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, W96, ct_u, ct_status, w_aff);
+    return hipGetLastError();
+}
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
-                                  const uint8_t* W96, uint32_t* ct_u, int32_t* ct_status, uint32_t* coefH,
-                                  uint32_t* coefW, uint8_t* vdig, hipStream_t st) {
-    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare(n, U48, V, V_off, W96, ct_u, ct_status, coefH, coefW, vdig, st));
+                                  const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare(n, U48, V, V_off, ct_status, coefH, vdig, st));
     hipError_t e = launch_tdec_v_digest(n, V, V_off, vdig, st);
     if (e != hipSuccess) return e;
     HBG_COUNT_MARK("tdec_ct_prepare", st);
-    tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, vdig, W96, ct_u, ct_status, coefH,
-                                                              coefW);
+    tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, vdig, ct_status, coefH);
     return hipGetLastError();
 }
-hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, int32_t* w_status,
-                                    uint32_t* coefW, hipStream_t st) {
-    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare_w(n, W96, ct_u, w_status, coefW, st));
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint32_t* w_aff, const uint32_t* ct_u,
+                                    const int32_t* ct_status, uint32_t* coefW, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare_w(n, w_aff, ct_u, ct_status, coefW, st));
     HBG_COUNT_MARK("tdec_ct_prepare_w", st);
     if (n == 0) return hipSuccess;
-    tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, W96, ct_u, w_status, coefW);
-    return hipGetLastError();
-}
-hipError_t launch_tdec_status_or(uint32_t n, int32_t* status, const int32_t* other, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    tdec_status_or<<<dim3((n + 255) / 256), dim3(256), 0, st>>>(n, status, other);
+    tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, w_aff, ct_u, ct_status, coefW);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
