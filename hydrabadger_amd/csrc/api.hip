@@ -396,6 +396,8 @@ static int switch_stream(hbg_ctx* c, hipStream_t s) {
 // c->stream continues after everything enqueued on c->aux.  For independent,
 // latency-bound launches of one call (few items: each kernel fills a few waves).
 static int fork_aux(hbg_ctx* c) {
+    // default priority: a high-priority aux stream let Ciphertext::verify take
+    // SIMDs from the check round the next rounds wait for (+32 ms, r05w)
     if (!c->aux) HBG_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     if (!c->fork_ev) HBG_TRY(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
     if (!c->join_ev) HBG_TRY(hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
@@ -677,6 +679,7 @@ namespace {
 struct CtTable {
     uint32_t *ct_u, *coefH, *coefW;
     int32_t* ct_status;  // [n_ct + 1]: entry n_ct is the invalid sentinel (device-mode index check)
+    int32_t* u_status;   // [n_ct + 1]: U's decode alone (the share leaves; ct_status once the lines are waited for)
     const uint8_t* U48;  // device copy of the compressed U points (batch weights hash them)
 };
 
@@ -713,21 +716,26 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     t.U48 = dU;
     t.coefH = (uint32_t*)ph;
     t.coefW = (uint32_t*)pwc;
-    HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
-    void *pdg, *pwa;
+    void *pdg, *pus;
     HBG_CHECK(scratch(c, 40, 32ull * n_ct, &pdg));
-    HBG_CHECK(scratch(c, 50, (size_t)bls::kWAffBytes * n_ct, &pwa));
-    // U, W decode (the status the share leaves read) here; H = hash_g1_g2(U, V)
-    // and both line tables on the aux stream, which the caller joins (or, with
-    // defer_lines, waits for through wait_lines before the first pairing, so
-    // the tables build beside the share leaves)
-    HBG_TRY(bls::launch_tdec_ct_decode(n_ct, dU, dW, t.ct_u, t.ct_status, (uint32_t*)pwa, c->stream));
+    HBG_CHECK(scratch(c, 50, 4ull * (n_ct + 1), &pus));
+    t.u_status = (int32_t*)pus;
+    HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
+    HBG_TRY(hipMemsetAsync(t.u_status + n_ct, 0xFF, 4, c->stream));
+    // U's decode (the status the share leaves read), then H = hash_g1_g2(U, V)
+    // and its lines here, while W's decode (the final status) and its lines run
+    // on the aux stream, which the caller joins (or, with defer_lines, waits for
+    // through wait_lines before the first pairing: beside H, the key tables
+    // and the share leaves).  H stays on this stream: a one-wave-per-SIMD
+    // launch on the aux stream gets no SIMD while the leaves hold them all
+    // (measured: H's 40 ms stretched over the whole 320 ms leaves launch).
+    HBG_TRY(bls::launch_tdec_ct_decode(n_ct, dU, t.ct_u, t.u_status, c->stream));
     HBG_CHECK(fork_aux(c));
     AuxJoin guard{defer_lines ? nullptr : c};  // deferred: the caller's guard joins
-    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, (const uint32_t*)pwa, t.ct_u, t.ct_status, t.coefW, c->aux));
-    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, t.ct_status, t.coefH, (uint8_t*)pdg, c->aux));
+    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, t.u_status, t.ct_status, t.coefW, c->aux));
     if (!c->lines_ev) HBG_TRY(hipEventCreateWithFlags(&c->lines_ev, hipEventDisableTiming));
     HBG_TRY(hipEventRecord(c->lines_ev, c->aux));
+    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, t.u_status, t.coefH, (uint8_t*)pdg, c->stream));
     if (!defer_lines) HBG_CHECK(join_aux(c));
     return HBG_OK;
 }
@@ -860,7 +868,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     }
 #endif
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
-    HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.ct_status, paff, pst, tbl,
+    HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.u_status, paff, pst, tbl,
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
     if (after_leaves) HBG_CHECK(after_leaves());
@@ -868,7 +876,8 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
     // round 0: every batch sum; a failing batch's value and its left half go to round 1
     auto list = [&](int r) { return (bls::BinItem*)((r & 1) ? items : items2); };  // round r's items (r >= 1)
     auto gts = [&](int r) { return (uint32_t*)(r == 0 ? gt0 : ((r & 1) ? gta : gtb)); };  // written by round r
-    HBG_TRY(bls::launch_tdec_bin_root(nb, counts + 3, ds, pm, sm, lk, t.ct_u, t.coefH, t.coefW, dok, gts(0), list(1),
+    HBG_TRY(bls::launch_tdec_bin_root(nb, counts + 3, ds, pm, sm, lk, t.ct_status, t.ct_u, t.coefH, t.coefW, dok, gts(0),
+                                      list(1),
                                       counts + 4, cap, (uint32_t*)fails, counts + 1, c->stream));
     HBG_DBG_STEP(c, "binary round 0");
     // rounds 1..6 (halves .. single shares): check the left child, derive the right
@@ -1023,7 +1032,7 @@ int hbg_tdec_combine(hbg_ctx* c, uint32_t t, uint32_t n_ct, const uint8_t* share
         dst = (int32_t*)s;
     }
     void *scr, *sds;
-    HBG_CHECK(scratch(c, 6, 4ull * 32 * m * n_ct, &scr));
+    HBG_CHECK(scratch(c, 6, 4ull * (32 * m > 36 ? 32 * m : 36) * n_ct, &scr));  // combine: >= one Jacobian sum per ct
     HBG_CHECK(scratch(c, 41, 32ull * n_ct, &sds));
     HBG_TRY(bls::launch_tdec_combine(n_ct, t, dsh, dix, dV, dVoff, dout, dst, (uint32_t*)scr, (uint8_t*)sds,
                                      c->stream));
@@ -1143,7 +1152,7 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
                                     c->stream));
     // PublicKeySet::decrypt (interpolate + xor_with_hash) of the selections
     void *scr, *sds;
-    HBG_CHECK(scratch(c, 39, 4ull * 32 * m * n_ct, &scr));
+    HBG_CHECK(scratch(c, 39, 4ull * (32 * m > 36 ? 32 * m : 36) * n_ct, &scr));
     HBG_CHECK(scratch(c, 41, 32ull * n_ct, &sds));
     HBG_TRY(bls::launch_tdec_combine(n_ct, t, s48, sidx, dV, dVoff, (uint8_t*)dpt, (int32_t*)dst, (uint32_t*)scr,
                                      (uint8_t*)sds, c->stream, (const uint32_t*)saff, n_nodes, sst));

@@ -24,16 +24,16 @@ constexpr uint32_t kSigBatchSumBytes = 21 * (36 + 72) * 4;  // per batch: G1 + G
 // their per-lane scratch (G2Prepared lines) is sized for kResidentBlocks * 64.
 constexpr uint32_t kResidentBlocks = 2048;
 
-// Ciphertext table: tdec_ct_decode (U, W + subgroup checks -> ct_u, ct_status,
-// w_aff [n][kWAffBytes / 4]), then H's and W's G2Prepared lines (ct_prepare:
-// vdig [n][32] scratch for SHA3(V) of the items with |V| > 64; ct_prepare_w).
-constexpr uint32_t kWAffBytes = 48 * 4;
-hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, const uint8_t* W96, uint32_t* ct_u,
-                                 int32_t* ct_status, uint32_t* w_aff, hipStream_t st);
+// Ciphertext table: tdec_ct_decode (U + subgroup check -> ct_u, u_status:
+// what the share leaves read), tdec_ct_prepare (H = hash_g1_g2(U, V) and its
+// lines for U-valid ciphertexts; vdig [n][32] scratch for SHA3(V) of the
+// items with |V| > 64) and, on a second stream, tdec_ct_prepare_w (W +
+// subgroup check -> the final ct_status, W's G2Prepared lines).
+hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, uint32_t* ct_u, int32_t* u_status, hipStream_t st);
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st);
-hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint32_t* w_aff, const uint32_t* ct_u,
-                                    const int32_t* ct_status, uint32_t* coefW, hipStream_t st);
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status,
+                                    int32_t* ct_status, uint32_t* coefW, hipStream_t st);
 // xor_with_hash's keystream: out = in ^ keystream(seeds[k]) per item (status[k] != 0: skipped; nullable)
 hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uint8_t* in, const uint64_t* off,
                                      uint8_t* out, const int32_t* status, hipStream_t st);
@@ -70,10 +70,10 @@ hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t*
 // gt_out / gt_in: 2 GT values per item of the writing / previous round.
 struct BinItem;
 hipError_t launch_tdec_bin_root(uint32_t cap, const uint32_t* nb_dev, const BatchDesc* desc, const uint32_t* perm,
-                                const uint32_t* sums, const uint8_t* leaf_ok, const uint32_t* ct_u,
-                                const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok, uint32_t* gt_out,
-                                BinItem* next, uint32_t* next_n, uint32_t next_cap, uint32_t* fail_list,
-                                uint32_t* fail_n, hipStream_t st);
+                                const uint32_t* sums, const uint8_t* leaf_ok, const int32_t* ct_status,
+                                const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
+                                uint32_t* gt_out, BinItem* next, uint32_t* next_n, uint32_t next_cap,
+                                uint32_t* fail_list, uint32_t* fail_n, hipStream_t st);
 hipError_t launch_tdec_bin_step(uint32_t cap, const uint32_t* n_dev, const BinItem* items, const BatchDesc* desc,
                                 const uint32_t* perm, const uint32_t* sums, const uint8_t* leaf_ok,
                                 const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,

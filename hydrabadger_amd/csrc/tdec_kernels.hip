@@ -953,37 +953,44 @@ BD Fp12 pairing_value2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2,
 }
 
 // ------------------------------------------------------------------ kernels
-// Ciphertext preparation in two halves (round 5): tdec_ct_decode — U and W
-// decoded with their subgroup checks: the ciphertext's status, U's affine
-// record and W's affine point, all that the share leaves need — then, on the
-// second stream and overlapped with the leaves, the expensive half: H =
-// hash_g1_g2(U, V) (SHA3(V) for |V| > 64, try-and-increment, cofactor
-// clearing) and both G2Prepared line tables (tdec_ct_prepare, _w), which only
-// the check rounds and Ciphertext::verify read.
-constexpr uint32_t kWAffWords = 48;  // W affine: x.c0 x.c1 y.c0 y.c1
-TDEC_WAVE1_KERNEL void tdec_ct_decode(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ W96,
-                                      uint32_t* __restrict__ ct_u, int32_t* __restrict__ ct_status,
-                                      uint32_t* __restrict__ w_aff) {
+// Ciphertext preparation (round 5): tdec_ct_decode — U decoded with its
+// subgroup check: U's affine record and U's status, all that the share leaves
+// read; H = hash_g1_g2(U, V) (SHA3(V) for |V| > 64, try-and-increment,
+// cofactor clearing) and its G2Prepared lines (tdec_ct_prepare); on the
+// second stream, beside H and the share leaves, W decoded with its subgroup
+// check (the final status: U's, else W's) and its lines (tdec_ct_prepare_w),
+// which only the check rounds and Ciphertext::verify read, after the
+// caller's wait for them.
+TDEC_KERNEL void tdec_ct_decode(uint32_t n, const uint8_t* __restrict__ U48, uint32_t* __restrict__ ct_u,
+                                int32_t* __restrict__ u_status) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     G1A u;
-    G2A w;
     const bool u_ok = g1_decompress(U48 + 48ull * k, u, true);
-    const bool w_ok = g2_decompress(W96 + 96ull * k, w, true);
     uint32_t* cu = ct_u + 32ull * k;
     store_fp(cu, u.x);
     store_fp(cu + 12, u.y);
     cu[24] = u.inf ? 1u : 0u;
-    cu[25] = w.inf ? 1u : 0u;
-    uint32_t* wa = w_aff + (uint64_t)kWAffWords * k;
-    store_fp(wa, w.x.c0);
-    store_fp(wa + 12, w.x.c1);
-    store_fp(wa + 24, w.y.c0);
-    store_fp(wa + 36, w.y.c1);
-    ct_status[k] = u_ok && w_ok ? 0 : HBG_E_INVALID_POINT;
+    u_status[k] = u_ok ? 0 : HBG_E_INVALID_POINT;
 }
 
-// H = hash_g1_g2(U, V) and its G2Prepared lines, for the decodable ciphertexts
+// W: decode + subgroup check, the ciphertext's final status, W's lines
+TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
+                                         const int32_t* __restrict__ u_status, int32_t* __restrict__ ct_status,
+                                         uint32_t* __restrict__ coefW) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    G2A w;
+    const bool w_ok = g2_decompress(W96 + 96ull * k, w, true);
+    ct_u[32ull * k + 25] = w.inf ? 1u : 0u;
+    const int32_t us = u_status[k];
+    const int32_t st = us != 0 ? us : (w_ok ? 0 : HBG_E_INVALID_POINT);
+    ct_status[k] = st;
+    if (st == 0 && !w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
+}
+
+// H = hash_g1_g2(U, V) and its G2Prepared lines, for the ciphertexts whose U
+// decodes (status: U's; a ciphertext whose W fails too gets an unused H)
 TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ V,
                                        const uint64_t* __restrict__ V_off, const uint8_t* __restrict__ vdig,
                                        const int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH) {
@@ -997,17 +1004,6 @@ TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U
     sha3_bytes(m, ml, seed);
     const G2A h = hash_g2_from_seed(seed);
     g2_prepare(h.x, h.y, coefH + (uint64_t)k * 72 * kMillerSteps);
-}
-
-// W's G2Prepared lines (W decoded by tdec_ct_decode)
-TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint32_t* __restrict__ w_aff,
-                                         const uint32_t* __restrict__ ct_u, const int32_t* __restrict__ ct_status,
-                                         uint32_t* __restrict__ coefW) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n || ct_status[k] != 0 || ct_u[32ull * k + 25] != 0) return;
-    const uint32_t* wa = w_aff + (uint64_t)kWAffWords * k;
-    g2_prepare({load_fp(wa), load_fp(wa + 12)}, {load_fp(wa + 24), load_fp(wa + 36)},
-               coefW + (uint64_t)k * 72 * kMillerSteps);
 }
 
 // Affine record (kAffWords words: x[12] y[12] inf): pk tables and the
@@ -1246,6 +1242,8 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
                                                         const uint32_t* __restrict__ pk_tbl,
                                                         uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok,
                                                         uint32_t* __restrict__ share_aff) {
+    // ct_status: U's decode status (the ciphertext table's final status, W's
+    // decode included, is applied by the root round)
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (b >= dev_count(nb_dev, cap)) return;  // grid sized for the bound; the batch count is a device word
@@ -1428,6 +1426,7 @@ BD void bin_node_verdict(uint32_t h, bool pass, const Fp12& v, uint32_t b, const
 TDEC_WAVE1_KERNEL void tdec_bin_root(uint32_t cap, const uint32_t* __restrict__ nb_dev,
                                      const BatchDesc* __restrict__ desc, const uint32_t* __restrict__ perm,
                                      const uint32_t* __restrict__ sums, const uint8_t* __restrict__ leaf_ok,
+                                     const int32_t* __restrict__ ct_status,
                                      const uint32_t* __restrict__ ct_u, const uint32_t* __restrict__ coefH,
                                      const uint32_t* __restrict__ coefW, uint8_t* __restrict__ ok,
                                      uint32_t* __restrict__ gt_out, BinItem* __restrict__ next,
@@ -1440,6 +1439,9 @@ TDEC_WAVE1_KERNEL void tdec_bin_root(uint32_t cap, const uint32_t* __restrict__ 
 #ifdef HBG_DEBUG_CHECKS
     if (!HBG_DBG_RANGE(d.end, g_dbg[0] + 1, "root d.end") || !HBG_DBG_RANGE(d.ct, g_dbg[2], "root d.ct")) return;
 #endif
+    // the leaves saw U's status only: a ciphertext whose W failed to decode has
+    // no lines and every share of it stays 0
+    if (ct_status[d.ct] != 0) return;
     const uint8_t* lok = leaf_ok + (uint64_t)b * kBatchShares;
     if (!node_any_valid(lok, 0, kBatchShares)) return;  // nothing valid to vouch for: those shares stay 0
     const Fp12 v = bin_node_value(sums, b, 0, d, ct_u, coefH, coefW);
@@ -1903,7 +1905,7 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
 // double-and-add: 317 -> 231 ms per 100 k ciphertexts, profiles/r03z).
 template <int G, int MMAX>
 TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
-                                  const uint32_t* __restrict__ idx, uint8_t* __restrict__ seeds,
+                                  const uint32_t* __restrict__ idx, uint32_t* __restrict__ sums,
                                   int32_t* __restrict__ status, const uint32_t* __restrict__ share_aff,
                                   uint32_t n_nodes, const int32_t* __restrict__ pre_status) {
     static_assert(G == 16 || G == 32 || G == 64, "a quarter, half or whole wave per ciphertext");
@@ -2025,11 +2027,21 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
     }
     if (!live || i != 0) return;
     status[g] = st;
-    if (st != 0) return;
-    const G1A sum = g1_to_affine(L);
+    if (st == 0) store_jac(sums + 36ull * g, L);  // affine + compress + SHA3: tdec_combine_seed
+}
+
+// The combination's epilogue, one lane per ciphertext: the Jacobian sum to
+// affine (one field inversion), compressed, SHA3 -> xor_with_hash's key (the
+// keystream runs in tdec_keystream_xor).  In the MSM kernel only each group's
+// first lane did this, 4 of 64 lanes busy through the inversion.
+TDEC_KERNEL void tdec_combine_seed(uint32_t n, const uint32_t* __restrict__ sums,
+                                   const int32_t* __restrict__ status, uint8_t* __restrict__ seeds) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || status[k] != 0) return;
+    const G1A sum = g1_to_affine(load_jac(sums + 36ull * k));
     uint8_t cg[48];
     g1_compress(cg, sum);
-    sha3_bytes(cg, 48, seeds + 32ull * g);  // xor_with_hash's key: the keystream runs in tdec_keystream_xor
+    sha3_bytes(cg, 48, seeds + 32ull * k);
 }
 
 // ------------------------------------------------------------------ SURVEY.md §8(f1)/(f2)
@@ -2710,12 +2722,11 @@ TDEC_WAVE1_KERNEL void tdec_test(int op, uint32_t n, const uint32_t* __restrict_
 #else
 }  // namespace bls
 namespace bls_lat {
-hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, const uint8_t* W96, uint32_t* ct_u,
-                                 int32_t* ct_status, uint32_t* w_aff, hipStream_t st);
+hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, uint32_t* ct_u, int32_t* u_status, hipStream_t st);
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st);
-hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint32_t* w_aff, const uint32_t* ct_u,
-                                    const int32_t* ct_status, uint32_t* coefW, hipStream_t st);
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status,
+                                    int32_t* ct_status, uint32_t* coefW, hipStream_t st);
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st);
 hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
@@ -2829,12 +2840,11 @@ hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uin
                                                                                              out, status);
     return hipGetLastError();
 }
-hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, const uint8_t* W96, uint32_t* ct_u,
-                                 int32_t* ct_status, uint32_t* w_aff, hipStream_t st) {
-    HBG_LAT_DISPATCH(n, launch_tdec_ct_decode(n, U48, W96, ct_u, ct_status, w_aff, st));
+hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, uint32_t* ct_u, int32_t* u_status, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_decode(n, U48, ct_u, u_status, st));
     HBG_COUNT_MARK("tdec_ct_decode", st);
     if (n == 0) return hipSuccess;
-    tdec_ct_decode<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, W96, ct_u, ct_status, w_aff);
+    tdec_ct_decode<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, ct_u, u_status);
     return hipGetLastError();
 }
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
@@ -2846,12 +2856,12 @@ hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t*
     tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, vdig, ct_status, coefH);
     return hipGetLastError();
 }
-hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint32_t* w_aff, const uint32_t* ct_u,
-                                    const int32_t* ct_status, uint32_t* coefW, hipStream_t st) {
-    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare_w(n, w_aff, ct_u, ct_status, coefW, st));
+hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status,
+                                    int32_t* ct_status, uint32_t* coefW, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare_w(n, W96, ct_u, u_status, ct_status, coefW, st));
     HBG_COUNT_MARK("tdec_ct_prepare_w", st);
     if (n == 0) return hipSuccess;
-    tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, w_aff, ct_u, ct_status, coefW);
+    tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, W96, ct_u, u_status, ct_status, coefW);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
@@ -2968,14 +2978,14 @@ hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t*
 }
 
 hipError_t launch_tdec_bin_root(uint32_t cap, const uint32_t* nb_dev, const BatchDesc* desc, const uint32_t* perm,
-                                const uint32_t* sums, const uint8_t* leaf_ok, const uint32_t* ct_u,
-                                const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok, uint32_t* gt_out,
-                                BinItem* next, uint32_t* next_n, uint32_t next_cap, uint32_t* fail_list,
-                                uint32_t* fail_n, hipStream_t st) {
+                                const uint32_t* sums, const uint8_t* leaf_ok, const int32_t* ct_status,
+                                const uint32_t* ct_u, const uint32_t* coefH, const uint32_t* coefW, uint8_t* ok,
+                                uint32_t* gt_out, BinItem* next, uint32_t* next_n, uint32_t next_cap,
+                                uint32_t* fail_list, uint32_t* fail_n, hipStream_t st) {
     HBG_COUNT_MARK("tdec_bin_root", st);
     if (cap == 0) return hipSuccess;
-    tdec_bin_root<<<item_grid(cap), dim3(64), 0, st>>>(cap, nb_dev, desc, perm, sums, leaf_ok, ct_u, coefH, coefW, ok,
-                                                       gt_out, next, next_n, next_cap, fail_list, fail_n);
+    tdec_bin_root<<<item_grid(cap), dim3(64), 0, st>>>(cap, nb_dev, desc, perm, sums, leaf_ok, ct_status, ct_u, coefH,
+                                                       coefW, ok, gt_out, next, next_n, next_cap, fail_list, fail_n);
     return hipGetLastError();
 }
 hipError_t launch_tdec_bin_step(uint32_t cap, const uint32_t* n_dev, const BinItem* items, const BatchDesc* desc,
@@ -3030,19 +3040,25 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     HBG_GRID_CHECK(n, 64);  // every grid of this call, before the first launch
+    // scratch: >= 36 words per ciphertext (the MSM kernels' Jacobian sums)
     if (t + 1 <= 24)
-        tdec_combine_msm<16, 24><<<dim3((n + 3) / 4), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status,
+        tdec_combine_msm<16, 24><<<dim3((n + 3) / 4), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
                                                                          share_aff, n_nodes, pre_status);
     else if (t + 1 <= 32)
-        tdec_combine_msm<32, 32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status,
+        tdec_combine_msm<32, 32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
                                                                          share_aff, n_nodes, pre_status);
     else if (t + 1 <= 64)
-        tdec_combine_msm<64, 64><<<dim3(n), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, share_aff,
+        tdec_combine_msm<64, 64><<<dim3(n), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status, share_aff,
                                                                n_nodes, pre_status);
     else
         tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (t + 1 <= 64) {
+        tdec_combine_seed<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, scratch, status, seeds);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     // xor_with_hash(g, V) of every ciphertext whose combination succeeded
     return launch_tdec_keystream_xor(n, seeds, V, V_off, out, status, st);
 }
