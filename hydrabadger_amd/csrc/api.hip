@@ -732,8 +732,8 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     HBG_TRY(bls::launch_tdec_ct_decode(n_ct, dU, t.ct_u, t.u_status, c->stream));
     HBG_CHECK(fork_aux(c));
     AuxJoin guard{defer_lines ? nullptr : c};  // deferred: the caller's guard joins
-    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, t.u_status, t.ct_status, t.coefW, c->aux));
     if (!c->lines_ev) HBG_TRY(hipEventCreateWithFlags(&c->lines_ev, hipEventDisableTiming));
+    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, t.u_status, t.ct_status, t.coefW, c->aux));
     HBG_TRY(hipEventRecord(c->lines_ev, c->aux));
     HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, t.u_status, t.coefH, (uint8_t*)pdg, c->stream));
     if (!defer_lines) HBG_CHECK(join_aux(c));
@@ -779,7 +779,7 @@ bool use_batched(const hbg_ctx* c, uint64_t n) {
 // after_leaves (optional): enqueues work that should start once the leaves
 // are done (ThresholdDecrypt's Ciphertext::verify on the second stream, so it
 // shares the chip with the check rounds instead of stalling the leaves).
-int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uint8_t* dU48, uint32_t n,
+int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, CtTable& t, const uint8_t* dU48, uint32_t n,
                           uint32_t n_pk, const uint8_t* dsh, const uint32_t* dsc, const uint32_t* dsp,
                           const uint32_t* paff, const int32_t* pst, uint8_t* dok,
                           const std::function<int()>& after_leaves = {}, uint32_t* share_aff = nullptr) {
@@ -872,7 +872,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, const CtTable& t, const uin
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
     if (after_leaves) HBG_CHECK(after_leaves());
-    HBG_CHECK(wait_lines(c));  // H's and W's line tables (stage_ct, built beside the leaves)
+    HBG_CHECK(wait_lines(c));  // W's line table (stage_ct's aux stream, beside H and the leaves)
     // round 0: every batch sum; a failing batch's value and its left half go to round 1
     auto list = [&](int r) { return (bls::BinItem*)((r & 1) ? items : items2); };  // round r's items (r >= 1)
     auto gts = [&](int r) { return (uint32_t*)(r == 0 ? gt0 : ((r & 1) ? gta : gtb)); };  // written by round r

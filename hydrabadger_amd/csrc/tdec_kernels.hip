@@ -975,11 +975,8 @@ TDEC_KERNEL void tdec_ct_decode(uint32_t n, const uint8_t* __restrict__ U48, uin
 }
 
 // W: decode + subgroup check, the ciphertext's final status, W's lines
-TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
-                                         const int32_t* __restrict__ u_status, int32_t* __restrict__ ct_status,
-                                         uint32_t* __restrict__ coefW) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
+BD void ct_w_body(uint32_t k, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
+                  const int32_t* __restrict__ u_status, int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefW) {
     G2A w;
     const bool w_ok = g2_decompress(W96 + 96ull * k, w, true);
     ct_u[32ull * k + 25] = w.inf ? 1u : 0u;
@@ -988,22 +985,37 @@ TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__
     ct_status[k] = st;
     if (st == 0 && !w.inf) g2_prepare(w.x, w.y, coefW + (uint64_t)k * 72 * kMillerSteps);
 }
+TDEC_WAVE1_KERNEL void tdec_ct_prepare_w(uint32_t n, const uint8_t* __restrict__ W96, uint32_t* __restrict__ ct_u,
+                                         const int32_t* __restrict__ u_status, int32_t* __restrict__ ct_status,
+                                         uint32_t* __restrict__ coefW) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) ct_w_body(k, W96, ct_u, u_status, ct_status, coefW);
+}
 
 // H = hash_g1_g2(U, V) and its G2Prepared lines, for the ciphertexts whose U
-// decodes (status: U's; a ciphertext whose W fails too gets an unused H)
-TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ V,
-                                       const uint64_t* __restrict__ V_off, const uint8_t* __restrict__ vdig,
-                                       const int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n || ct_status[k] != 0) return;
+// decodes (status: U's; a ciphertext whose W fails too gets an unused H).
+// vdig: SHA3(V) of the items with |V| > 64 (tdec_v_digest), or null: hashed
+// here, one lane per item.
+BD void ct_h_body(uint32_t k, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ V,
+                  const uint64_t* __restrict__ V_off, const uint8_t* __restrict__ vdig,
+                  const int32_t* __restrict__ u_status, uint32_t* __restrict__ coefH) {
+    if (u_status[k] != 0) return;
     // H = hash_g1_g2(U, V): m = (|V| > 64 ? sha3(V) : V) || compress(U)
     const uint64_t off = V_off[k], len = V_off[k + 1] - off;
+    uint8_t dg[32];
+    if (!vdig && len > 64) sha3_long(V + off, len, dg);
     uint8_t m[64 + 48];
-    const uint32_t ml = hash_g1_g2_msg(V + off, len, vdig + 32ull * k, U48 + 48ull * k, m);
+    const uint32_t ml = hash_g1_g2_msg(V + off, len, vdig ? vdig + 32ull * k : dg, U48 + 48ull * k, m);
     uint8_t seed[32];
     sha3_bytes(m, ml, seed);
     const G2A h = hash_g2_from_seed(seed);
     g2_prepare(h.x, h.y, coefH + (uint64_t)k * 72 * kMillerSteps);
+}
+TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ V,
+                                       const uint64_t* __restrict__ V_off, const uint8_t* __restrict__ vdig,
+                                       const int32_t* __restrict__ u_status, uint32_t* __restrict__ coefH) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) ct_h_body(k, U48, V, V_off, vdig, u_status, coefH);
 }
 
 // Affine record (kAffWords words: x[12] y[12] inf): pk tables and the

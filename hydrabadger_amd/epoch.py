@@ -113,6 +113,11 @@ def arrival_orders_views(epoch: int, proposers, n: int, nodes, device=None) -> n
     ties by sender), evaluated as wrapping 64-bit tensor arithmetic (on
     `device` when given) instead of one Python call per key (a 128-node epoch
     has 128 x 128 x 128 keys)."""
+    return arrival_orders_views_t(epoch, proposers, n, nodes, device).cpu().numpy().astype(np.int64)
+
+
+def arrival_orders_views_t(epoch: int, proposers, n: int, nodes, device=None) -> torch.Tensor:
+    """arrival_orders_views as an int64 tensor on `device`."""
     ids = [[arrival_id(epoch, int(p), int(v)) ^ BASE_SEED ^ (TAG_ARRIVAL << 48) for p in proposers] for v in nodes]
     seed = torch.tensor([[_i64(x) for x in row] for row in ids], dtype=torch.int64, device=device)   # [v][k]
     z = seed.unsqueeze(-1) + _i64(GAMMA) * torch.arange(1, n + 1, dtype=torch.int64, device=device)
@@ -123,7 +128,7 @@ def arrival_orders_views(epoch: int, proposers, n: int, nodes, device=None) -> n
     z = (z ^ shr(z, 27)) * _i64(0x94D049BB133111EB)
     z = z ^ shr(z, 31)
     key = z ^ (-(1 << 63))  # u64 order as int64 order
-    return torch.sort(key, dim=-1, stable=True).indices.cpu().numpy().astype(np.int64)
+    return torch.sort(key, dim=-1, stable=True).indices
 
 
 @dataclass(frozen=True)
@@ -398,20 +403,20 @@ class HoneyBadgerEpoch:
             shares = e.decrypt_shares(U, sk_use, pc, pj).view(k, m, 48)
             sall = self._gather(shares.permute(1, 0, 2).contiguous())   # [N s][k][48]
             share48 = sall.permute(1, 0, 2).contiguous()                # [k][N][48]
-            silent = np.array([s in faults.silent for s in range(N)])
-            order = arrival_orders_views(epoch, acc, N, views, dev)         # [v][k][N]
+            # the arrival lists, built on the device ([v][k][N]: 2.1 M entries at N = 128)
+            silent = torch.tensor([s in faults.silent for s in range(N)], device=dev)
+            order = arrival_orders_views_t(epoch, acc, N, views, dev)       # [v][k][N]
             keep = ~silent[order]
             per_node = views[0] >= 0
-            vv = np.array(views, np.int64).reshape(-1, 1, 1)
+            vv = torch.tensor(views, dtype=torch.int64, device=dev).view(-1, 1, 1)
             if per_node:  # a node's own share is no network arrival: its start_decryption inserts it
                 keep &= order != vv
             # silent senders' entries dropped, the rest kept in arrival order, -1 padded
-            order = np.take_along_axis(order, np.argsort(~keep, axis=-1, kind="stable"), -1)
-            order[np.arange(N) >= keep.sum(-1, keepdims=True)] = -1
+            order = torch.take_along_dim(order, torch.argsort((~keep).to(torch.uint8), dim=-1, stable=True), -1)
+            order = torch.where(torch.arange(N, device=dev) < keep.sum(-1, keepdim=True), order, -1)
             if per_node:  # hbbft start_decryption at validator v (HBG_ARRIVAL_OWN | v) before any arrival
-                own = np.broadcast_to(np.int64(_lib.HBG_ARRIVAL_OWN) | vv, (nv, k, 1))
-                order = np.concatenate([own, order], -1)
-            arr = order.astype(np.int64).astype(np.uint32).view(np.int32)
+                order = torch.cat([(vv | _lib.HBG_ARRIVAL_OWN).expand(nv, k, 1), order], -1)
+            arr = torch.where(order >= 1 << 31, order - (1 << 32), order).to(torch.int32)  # u32 bits
             # view v's instance of ciphertext q: its own copy of (U, V, W) and the N shares
             sh = share48.repeat(nv, 1, 1).view(nv, k, N, 48)
             for vi, v in enumerate(views):
@@ -422,7 +427,7 @@ class HoneyBadgerEpoch:
             V_off = torch.arange(nv * k + 1, dtype=torch.int64, device=dev) * P
             pt, ct_status, outcome = e.threshold_decrypt(
                 self.t, N, U.repeat(nv, 1), V.repeat(nv, 1).reshape(-1), V_off, W.contiguous().repeat(nv, 1),
-                self.pk48, sh.reshape(nv * k, N, 48), torch.from_numpy(arr.reshape(nv * k, -1)).to(dev))
+                self.pk48, sh.reshape(nv * k, N, 48), arr.reshape(nv * k, -1).contiguous())
             plaintexts = pt.view(nv, k, P)
             ct_status = ct_status.view(nv, k)
             outcome = outcome.view(nv, k, N)
