@@ -231,7 +231,7 @@ def fp_per_share(prof: dict, key: str, n_shares: int) -> float:
 
 # Kernels of one hbg_tdec_threshold_decrypt call (the epoch generator's
 # encrypt / decrypt_share kernels in the same profile are not part of it).
-TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_decode", "tdec_ct_prepare", "tdec_ct_prepare_w", "tdec_v_digest",
+TDEC_DRIVER_KERNELS = ("tdec_pk_prepare", "tdec_ct_decode", "tdec_ct_prepare", "tdec_ct_prepare_w", "tdec_ct_prepare_hw", "tdec_v_digest",
                        "tdec_ct_verify", "tdec_pair_index", "tdec_pk_table", "tdec_iota", "tdec_group_marks",
                        "tdec_batch_heads", "tdec_batch_desc", "tdec_batch_leaves", "tdec_bin_root", "tdec_bin_step",
                        "tdec_verify_shares", "tdec_select", "tdec_combine_msm", "tdec_combine_seed",

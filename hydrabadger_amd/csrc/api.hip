@@ -681,7 +681,40 @@ struct CtTable {
     int32_t* ct_status;  // [n_ct + 1]: entry n_ct is the invalid sentinel (device-mode index check)
     int32_t* u_status;   // [n_ct + 1]: U's decode alone (the share leaves; ct_status once the lines are waited for)
     const uint8_t* U48;  // device copy of the compressed U points (batch weights hash them)
+    // launch_lines' inputs (stage_ct with defer_lines stops after U's decode)
+    uint32_t n_ct = 0;
+    const uint8_t *W96 = nullptr, *V = nullptr;
+    const uint64_t* V_off = nullptr;
+    uint8_t* vdig = nullptr;
+    bool lines_pending = false;
 };
+
+// Ciphertexts up to which H's sponge + lines (one lane per ciphertext, one
+// wave per SIMD) and W's lines run as one grid on the aux stream beside the
+// share leaves: both fit one wave round on half of the 1,024 SIMDs (the
+// configs[4] epoch's 16,384 ciphertexts per call).
+constexpr uint32_t kLinesBesideLeavesMax = 32768;
+constexpr uint32_t kLinesBesideLeavesMin = 8193;  // fewer: the wave sponge (v_digest, <= 8,192) and H on this stream
+
+// W's decode (the final status) and lines on the aux stream; H = hash_g1_g2(U, V)
+// and its lines on this stream — or (deferred, few thousand ciphertexts) both
+// in one grid on the aux stream with the sponge inline, so the share leaves
+// start at once.  Before the first pairing the stream waits (wait_lines).
+int launch_lines(hbg_ctx* c, CtTable& t, bool beside) {
+    t.lines_pending = false;
+    HBG_CHECK(fork_aux(c));
+    if (!c->lines_ev) HBG_TRY(hipEventCreateWithFlags(&c->lines_ev, hipEventDisableTiming));
+    if (beside && t.n_ct >= kLinesBesideLeavesMin && t.n_ct <= kLinesBesideLeavesMax) {
+        HBG_TRY(bls::launch_tdec_ct_prepare_hw(t.n_ct, t.U48, t.V, t.V_off, t.W96, t.ct_u, t.u_status, t.ct_status,
+                                               t.coefH, t.coefW, c->aux));
+        HBG_TRY(hipEventRecord(c->lines_ev, c->aux));
+        return HBG_OK;
+    }
+    HBG_TRY(bls::launch_tdec_ct_prepare_w(t.n_ct, t.W96, t.ct_u, t.u_status, t.ct_status, t.coefW, c->aux));
+    HBG_TRY(hipEventRecord(c->lines_ev, c->aux));
+    HBG_TRY(bls::launch_tdec_ct_prepare(t.n_ct, t.U48, t.V, t.V_off, t.u_status, t.coefH, t.vdig, c->stream));
+    return HBG_OK;
+}
 
 // Stage (host mode) and prepare a ciphertext table on the device.
 int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
@@ -722,25 +755,28 @@ int stage_ct(hbg_ctx* c, uint32_t n_ct, const uint8_t* U48, const uint8_t* V, co
     t.u_status = (int32_t*)pus;
     HBG_TRY(hipMemsetAsync(t.ct_status + n_ct, 0xFF, 4, c->stream));  // sentinel status = -1 (HBG_E_ARG)
     HBG_TRY(hipMemsetAsync(t.u_status + n_ct, 0xFF, 4, c->stream));
-    // U's decode (the status the share leaves read), then H = hash_g1_g2(U, V)
-    // and its lines here, while W's decode (the final status) and its lines run
-    // on the aux stream, which the caller joins (or, with defer_lines, waits for
-    // through wait_lines before the first pairing: beside H, the key tables
-    // and the share leaves).  H stays on this stream: a one-wave-per-SIMD
-    // launch on the aux stream gets no SIMD while the leaves hold them all
-    // (measured: H's 40 ms stretched over the whole 320 ms leaves launch).
+    // U's decode (the status the share leaves read) here; the line tables by
+    // launch_lines, now or (defer_lines: the batched verification) right
+    // before the share leaves, after the batch plan's sort, which stalls when
+    // one-wave-per-SIMD launches hold half the chip.  A one-wave-per-SIMD
+    // launch queued on a second stream behind other work gets no SIMD while
+    // the leaves hold them all (measured: H's 40 ms stretched over the whole
+    // 320 ms leaves launch), so the beside-the-leaves launches go first.
     HBG_TRY(bls::launch_tdec_ct_decode(n_ct, dU, t.ct_u, t.u_status, c->stream));
-    HBG_CHECK(fork_aux(c));
-    AuxJoin guard{defer_lines ? nullptr : c};  // deferred: the caller's guard joins
-    if (!c->lines_ev) HBG_TRY(hipEventCreateWithFlags(&c->lines_ev, hipEventDisableTiming));
-    HBG_TRY(bls::launch_tdec_ct_prepare_w(n_ct, dW, t.ct_u, t.u_status, t.ct_status, t.coefW, c->aux));
-    HBG_TRY(hipEventRecord(c->lines_ev, c->aux));
-    HBG_TRY(bls::launch_tdec_ct_prepare(n_ct, dU, *dV, *dVoff, t.u_status, t.coefH, (uint8_t*)pdg, c->stream));
-    if (!defer_lines) HBG_CHECK(join_aux(c));
+    t.n_ct = n_ct;
+    t.W96 = dW;
+    t.V = *dV;
+    t.V_off = *dVoff;
+    t.vdig = (uint8_t*)pdg;
+    t.lines_pending = true;
+    if (defer_lines) return HBG_OK;  // the caller's guard joins
+    AuxJoin guard{c};
+    HBG_CHECK(launch_lines(c, t, false));
+    HBG_CHECK(join_aux(c));
     return HBG_OK;
 }
 
-// The stream waits for stage_ct's line tables (not for later aux work).
+// The stream waits for the ciphertext line tables (not for later aux work).
 int wait_lines(hbg_ctx* c) {
     HBG_TRY(hipStreamWaitEvent(c->stream, c->lines_ev, 0));
     return HBG_OK;
@@ -787,14 +823,6 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, CtTable& t, const uint8_t* 
         void* p;
         HBG_CHECK(scratch(c, 46, 4ull * bls::kAffWords * n, &p));
         share_aff = (uint32_t*)p;
-    }
-    uint32_t* tbl = nullptr;
-    if (c->tdec_batched == 2 || (uint64_t)n >= kPkTableMinUses * n_pk) {
-        void* p;
-        HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
-        tbl = (uint32_t*)p;
-        HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream));
-        HBG_DBG_STEP(c, "pk_table");
     }
     const uint32_t n_keys = n_ct + 1;  // + the sentinel ciphertext
     void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
@@ -867,12 +895,23 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, CtTable& t, const uint8_t* 
         if (bad || hnb[0] > nb) return HBG_E_DEVICE;
     }
 #endif
+    // the line tables (deferred by stage_ct) before the key table: their
+    // one-wave-per-SIMD grid is resident before the leaves' grid is queued
+    if (t.lines_pending) HBG_CHECK(launch_lines(c, t, true));
+    uint32_t* tbl = nullptr;
+    if (c->tdec_batched == 2 || (uint64_t)n >= kPkTableMinUses * n_pk) {
+        void* p;
+        HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
+        tbl = (uint32_t*)p;
+        HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream));
+        HBG_DBG_STEP(c, "pk_table");
+    }
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.u_status, paff, pst, tbl,
                                           (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
+    HBG_CHECK(wait_lines(c));  // the line tables (launch_lines: beside the leaves)
     if (after_leaves) HBG_CHECK(after_leaves());
-    HBG_CHECK(wait_lines(c));  // W's line table (stage_ct's aux stream, beside H and the leaves)
     // round 0: every batch sum; a failing batch's value and its left half go to round 1
     auto list = [&](int r) { return (bls::BinItem*)((r & 1) ? items : items2); };  // round r's items (r >= 1)
     auto gts = [&](int r) { return (uint32_t*)(r == 0 ? gt0 : ((r & 1) ? gta : gtb)); };  // written by round r

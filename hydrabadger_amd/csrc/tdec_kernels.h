@@ -34,6 +34,10 @@ hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t*
                                   const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st);
 hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status,
                                     int32_t* ct_status, uint32_t* coefW, hipStream_t st);
+// H (sponge inline) and W's preparation in one grid (the two above, concurrent)
+hipError_t launch_tdec_ct_prepare_hw(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                                     const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status, int32_t* ct_status,
+                                     uint32_t* coefH, uint32_t* coefW, hipStream_t st);
 // xor_with_hash's keystream: out = in ^ keystream(seeds[k]) per item (status[k] != 0: skipped; nullable)
 hipError_t launch_tdec_keystream_xor(uint64_t n, const uint8_t* seeds, const uint8_t* in, const uint64_t* off,
                                      uint8_t* out, const int32_t* status, hipStream_t st);

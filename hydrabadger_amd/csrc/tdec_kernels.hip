@@ -1018,6 +1018,26 @@ TDEC_WAVE1_KERNEL void tdec_ct_prepare(uint32_t n, const uint8_t* __restrict__ U
     if (k < n) ct_h_body(k, U48, V, V_off, vdig, u_status, coefH);
 }
 
+// H (sponge inline) and W in ONE launch, for the batched schedule's few
+// thousand ciphertexts (api.hip launch_lines): blocks [0, nb) build H's lines,
+// [nb, 2 nb) W's.  Launched beside the share leaves; as two launches on two
+// extra streams the second sat behind the first (the runtime put both streams
+// on one hardware queue), so one grid keeps the two concurrent.
+TDEC_WAVE1_KERNEL void tdec_ct_prepare_hw(uint32_t n, const uint8_t* __restrict__ U48, const uint8_t* __restrict__ V,
+                                          const uint64_t* __restrict__ V_off, const uint8_t* __restrict__ W96,
+                                          uint32_t* __restrict__ ct_u, const int32_t* __restrict__ u_status,
+                                          int32_t* __restrict__ ct_status, uint32_t* __restrict__ coefH,
+                                          uint32_t* __restrict__ coefW) {
+    const uint32_t nb = (n + 63) / 64;
+    if (blockIdx.x < nb) {
+        const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+        if (k < n) ct_h_body(k, U48, V, V_off, nullptr, u_status, coefH);
+    } else {
+        const uint32_t k = (blockIdx.x - nb) * blockDim.x + threadIdx.x;
+        if (k < n) ct_w_body(k, W96, ct_u, u_status, ct_status, coefW);
+    }
+}
+
 // Affine record (kAffWords words: x[12] y[12] inf): pk tables and the
 // verified-share table the combine reads.
 BD void store_aff(uint32_t* d, const G1A& p) {
@@ -1897,7 +1917,7 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
 
 // PublicKeySet::decrypt as a bucket multi-scalar multiplication per G-lane
 // group (G = 16: four ciphertexts per wave, t + 1 <= 24, lane i owning shares
-// i and i + 16; G = 32: two, t + 1 <= 32; G = 64: one, t + 1 <= 64); same
+// i and i + 16; G = 32: two, t + 1 <= 32 or, two shares a lane, <= 64); same
 // sum, same error precedence (DuplicateEntry before an undecodable share) as
 // the one-lane-per-ciphertext tdec_combine (kept for t + 1 > 64):
 //  1. per owned share: DuplicateEntry / decode checks (or, inside
@@ -1925,7 +1945,12 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
     constexpr uint32_t GPB = 64 / G;                 // groups per 64-lane block
     constexpr uint32_t kPer = 64 / G;                // 2-bit windows per lane (the last lane: one more)
     constexpr uint32_t SPL = (MMAX + G - 1) / G;     // shares per lane
-    __shared__ uint32_t sPt[GPB][MMAX][36];          // S_i: x, y, beta x ([x^2]S_i = (beta x, -y))
+    // beta x kept in LDS, except where it would cost occupancy (more than
+    // 20 KB a block leaves fewer than 8 blocks a CU — <32, 64>: 23 KB; beta x
+    // is then recomputed per use)
+    constexpr bool kBetaLds = GPB * MMAX * (36 * 4 + 2 * 5 * 4) <= 20480;
+    constexpr uint32_t kPtWords = kBetaLds ? 36 : 24;
+    __shared__ uint32_t sPt[GPB][MMAX][kPtWords];    // S_i: x, y, beta x ([x^2]S_i = (beta x, -y))
     __shared__ uint32_t sSc[GPB][2 * MMAX][5];       // point 2i: rm_i (S_i); 2i + 1: q_i ([x^2]S_i)
     const uint32_t gl = threadIdx.x / G, i = threadIdx.x % G, gshift = gl * G;
     const uint32_t g = blockIdx.x * GPB + gl;
@@ -1987,7 +2012,7 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
             uint32_t* a = sPt[gl][sI];
             store_fp(a, p[r].x);
             store_fp(a + 12, p[r].y);
-            store_fp(a + 24, fp_mul(p[r].x, fp_const(kBeta)));
+            if (kBetaLds) store_fp(a + 24, fp_mul(p[r].x, fp_const(kBeta)));
 #pragma unroll
             for (int w = 0; w < 5; ++w) {
                 sSc[gl][2 * sI][w] = rm[w];
@@ -2009,7 +2034,9 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
             const uint32_t d = (sSc[gl][j][word] >> sh) & 3u;
             if (!__any(d != 0)) continue;  // wave-uniform skip (no lane has this digit)
             const uint32_t* pt = sPt[gl][j >> 1];
-            const Fp px = load_fp(pt + ((j & 1u) ? 24 : 0));
+            Fp px;
+            if (kBetaLds) px = load_fp(pt + ((j & 1u) ? 24 : 0));
+            else px = (j & 1u) ? fp_mul(load_fp(pt), fp_const(kBeta)) : load_fp(pt);
             Fp py = load_fp(pt + 12);
             if (j & 1u) py = fp_neg(py);
             const G1 sel = d == 1u ? b1 : (d == 2u ? b2 : b3);
@@ -2739,6 +2766,9 @@ hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t*
                                   const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st);
 hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status,
                                     int32_t* ct_status, uint32_t* coefW, hipStream_t st);
+hipError_t launch_tdec_ct_prepare_hw(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                                     const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status, int32_t* ct_status,
+                                     uint32_t* coefH, uint32_t* coefW, hipStream_t st);
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
                                   hipStream_t st);
 hipError_t launch_tdec_verify_shares(uint64_t cap, const uint32_t* n_dev, const uint8_t* share48,
@@ -2862,8 +2892,10 @@ hipError_t launch_tdec_ct_decode(uint32_t n, const uint8_t* U48, uint32_t* ct_u,
 hipError_t launch_tdec_ct_prepare(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
                                   const int32_t* ct_status, uint32_t* coefH, uint8_t* vdig, hipStream_t st) {
     HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare(n, U48, V, V_off, ct_status, coefH, vdig, st));
-    hipError_t e = launch_tdec_v_digest(n, V, V_off, vdig, st);
-    if (e != hipSuccess) return e;
+    if (vdig) {  // else the sponge runs inline, one lane per ciphertext
+        hipError_t e = launch_tdec_v_digest(n, V, V_off, vdig, st);
+        if (e != hipSuccess) return e;
+    }
     HBG_COUNT_MARK("tdec_ct_prepare", st);
     tdec_ct_prepare<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, U48, V, V_off, vdig, ct_status, coefH);
     return hipGetLastError();
@@ -2874,6 +2906,16 @@ hipError_t launch_tdec_ct_prepare_w(uint32_t n, const uint8_t* W96, uint32_t* ct
     HBG_COUNT_MARK("tdec_ct_prepare_w", st);
     if (n == 0) return hipSuccess;
     tdec_ct_prepare_w<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, W96, ct_u, u_status, ct_status, coefW);
+    return hipGetLastError();
+}
+hipError_t launch_tdec_ct_prepare_hw(uint32_t n, const uint8_t* U48, const uint8_t* V, const uint64_t* V_off,
+                                     const uint8_t* W96, uint32_t* ct_u, const int32_t* u_status, int32_t* ct_status,
+                                     uint32_t* coefH, uint32_t* coefW, hipStream_t st) {
+    HBG_LAT_DISPATCH(n, launch_tdec_ct_prepare_hw(n, U48, V, V_off, W96, ct_u, u_status, ct_status, coefH, coefW, st));
+    HBG_COUNT_MARK("tdec_ct_prepare_hw", st);
+    if (n == 0) return hipSuccess;
+    tdec_ct_prepare_hw<<<dim3(2 * ((n + 63) / 64)), dim3(64), 0, st>>>(n, U48, V, V_off, W96, ct_u, u_status,
+                                                                       ct_status, coefH, coefW);
     return hipGetLastError();
 }
 hipError_t launch_tdec_pk_prepare(uint32_t n, const uint8_t* pk48, uint32_t* pk_aff, int32_t* pk_status,
@@ -3046,7 +3088,7 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff,
                                uint32_t n_nodes, const int32_t* pre_status) {
-    HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 24 ? 16u : (t + 1 <= 32 ? 32u : 64u)),
+    HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 24 ? 16u : 32u),
                      launch_tdec_combine(n, t, share48, idx, V, V_off, out, status, scratch, seeds, st, share_aff,
                                          n_nodes, pre_status));
     HBG_COUNT_MARK("tdec_combine", st);
@@ -3059,9 +3101,9 @@ hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, c
     else if (t + 1 <= 32)
         tdec_combine_msm<32, 32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
                                                                          share_aff, n_nodes, pre_status);
-    else if (t + 1 <= 64)
-        tdec_combine_msm<64, 64><<<dim3(n), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status, share_aff,
-                                                               n_nodes, pre_status);
+    else if (t + 1 <= 64)  // two shares a lane: ~28 % fewer Fp products per ciphertext than <64, 64> at t = 42
+        tdec_combine_msm<32, 64><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
+                                                                         share_aff, n_nodes, pre_status);
     else
         tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, scratch);
     hipError_t e = hipGetLastError();

@@ -300,6 +300,36 @@ def test_batched_verify_equals_per_share(bad_rate, seed):
         assert np.array_equal(o, expect)
 
 
+def test_batched_lines_beside_leaves():
+    """8,200 ciphertexts (the fixture's 4 replicated) x 64 shares, 1 % bad:
+    with 8,193..32,768 ciphertexts the batched schedule builds H (sponge
+    inline) and W's line tables in one grid beside the share leaves
+    (api.hip launch_lines, tdec_ct_prepare_hw); its bits equal the fixture's
+    per-share truth."""
+    import json
+    import os
+    from hydrabadger_amd import _lib
+    th = _th()
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tdec_n64.json")))["scenario"]
+    K, n = len(g["cts"]), len(g["pk_shares"])
+    n_ct = 8200
+    cts = [th.Ciphertext(bytes.fromhex(g["cts"][j % K]["U"]), bytes.fromhex(g["cts"][j % K]["V"]),
+                         bytes.fromhex(g["cts"][j % K]["W"])) for j in range(n_ct)]
+    pk = [bytes.fromhex(p) for p in g["pk_shares"]]
+    shares = [[bytes.fromhex(x) for x in c["shares"]] for c in g["cts"]]
+    rng = np.random.default_rng(11)
+    bad = rng.random(n_ct * n) < 0.01
+    items = [(shares[j % K][i], j, (i + 1) % n if bad[j * n + i] else i) for j in range(n_ct) for i in range(n)]
+    expect = (~bad).astype(np.uint8)
+    ctx = _lib.Context(0)
+    try:
+        _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, 2))
+        out = th.verify_shares_batch(cts, pk, items, ctx)
+    finally:
+        ctx.close()
+    assert np.array_equal(out, expect)
+
+
 def test_g1_mul_u64_and_add():
     """Device G1 scalar multiplication by 64-bit weights and Jacobian addition
     (the batched verifier's building blocks) against the oracle."""

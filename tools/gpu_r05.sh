@@ -33,6 +33,14 @@ for s in $STEPS; do
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
             python3 bench.py --steps 5 --warmup 2 > "$OUT/trace_bench.json" 2> "$OUT/trace.err" \
             || { tail -20 "$OUT/trace.err"; exit 5; } ;;
+    etrace)
+        timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/etrace" -o ep -- \
+            python3 bench.py --steps 2 --warmup 1 --instances 512 --no-cpu --no-decode --legs ${ELEGS:-epoch} \
+            > "$OUT/etrace_bench.json" 2> "$OUT/etrace.err" || { tail -20 "$OUT/etrace.err"; exit 8; }
+        python3 tools/itemise_trace.py "$(ls "$OUT"/etrace/*/ep_kernel_trace.csv "$OUT"/etrace/ep_kernel_trace.csv 2>/dev/null | head -1)" \
+            > "$OUT/epoch_itemised.txt" 2>&1 || true
+        tail -40 "$OUT/epoch_itemised.txt"
+        python3 tools/bench_summary.py "$OUT/etrace_bench.json" || true ;;
     probe)
         timeout -k 10 400 python3 -u tools/ctw_probe.py all ${PROBE_ARGS:-} > "$OUT/probe.log" 2>&1 \
             || { tail -60 "$OUT/probe.log"; exit 6; }
