@@ -27,6 +27,10 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+# option: rho rotations by a multiple of 8 (56 and 8: four funnel shifts a round) as
+# v_perm_b32 instead of the half-rate v_alignbit_b32
+BYTE_PERM = os.environ.get("KECCAK_BYTE_PERM", "0") == "1"  # measured slower (r05c1): off
+
 ROT = [[0, 36, 3, 41, 18], [1, 44, 10, 45, 2], [62, 6, 43, 15, 61], [28, 55, 25, 21, 56], [27, 20, 39, 8, 14]]
 # ROT[x][y]
 
@@ -115,6 +119,14 @@ def layout(hshift: int = 0):
             blo, bhi = B[dx][dy]
             if r == 0:
                 continue  # B[0,0] aliases A[0,0]
+            amt = 32 - r if r < 32 else 64 - r
+            if BYTE_PERM and amt % 8 == 0 and r != 32:
+                # a byte-multiple funnel shift as a full-rate v_perm_b32
+                # (selector from an SGPR: no VOP3 literal on gfx9)
+                s0, s1 = (lo, hi) if r < 32 else (hi, lo)
+                L.append(f"v_perm_b32 {v(blo)}, {v(s0)}, {v(s1)}, %[p{amt}]")
+                L.append(f"v_perm_b32 {v(bhi)}, {v(s1)}, {v(s0)}, %[p{amt}]")
+                continue
             if r < 32:
                 L.append(f"v_alignbit_b32 {v(blo)}, {v(lo)}, {v(hi)}, {32 - r}")
                 L.append(f"v_alignbit_b32 {v(bhi)}, {v(hi)}, {v(lo)}, {32 - r}")
@@ -199,7 +211,7 @@ def schedule(lines, lat=2, gap=2):
 
 def main():
     L, A, regs_used = layout()
-    if os.environ.get("KECCAK_SCHED", "1") == "1":
+    if os.environ.get("KECCAK_SCHED", "0") == "1":  # measured no faster: off
         L = schedule(L)
     nreg = max(regs_used) + 1
 
@@ -231,6 +243,7 @@ def main():
     state_regs = {A[x][y][h] for x in range(5) for y in range(5) for h in range(2)}
     clob = [f'"{v(i)}"' for i in regs_used if i not in state_regs]
     asm_text = "\\n\\t".join(asm_lines)
+    perm_ops = ', [p8] "s"(0x04030201u), [p24] "s"(0x06050403u)' if BYTE_PERM else ""
     hdr = f"""// Generated by tools/gen_keccak_asm.py — do not edit.
 // Keccak-f[1600] for gfx950 with a bank-conflict-aware VGPR layout (see the
 // generator's docstring).  Uses v0..v{nreg - 1}; state pinned to fixed VGPRs.
@@ -257,7 +270,7 @@ __device__ __forceinline__ void keccak_f_asm(u64p (&a)[25]) {{
     const uint32_t* tab4 = kKeccakRC_asm + 1;
     asm volatile("{asm_text}"
         : {", ".join(outs)}, [cnt] "=&s"(cnt), [rl] "=&s"(rl), [rh] "=&s"(rh)
-        : [tab] "s"(tab), [tab4] "s"(tab4)
+        : [tab] "s"(tab), [tab4] "s"(tab4){perm_ops}
         : {", ".join(clob)}, "scc", "memory");
 }}
 
