@@ -381,15 +381,18 @@ class HoneyBadgerEpoch:
         S = vals.shape[-1]
         sh = vals.view(N, N, S).permute(1, 0, 2).contiguous()  # [p][s][S]
         present = (holds & delivered.unsqueeze(2)).to(torch.uint8)   # [v][p][s]
-        outs, plens, dsts = [], [], []
+        D = bc.shard_counts(N)[0]
+        OS = (D * L + 15) // 16 * 16
+        out = e.zeros((nv, N, OS))                            # every view's decodes, written in place
+        plens, dsts = [], []
         for c0 in range(0, nv, decode_chunk):
             c = min(decode_chunk, nv - c0)
-            o, pl, ds = e.decode(N, L, _copies(sh, c), present[c0:c0 + c].reshape(c * N, N).contiguous(),
-                                 root_p[c0:c0 + c].reshape(c * N, 32).contiguous())
-            outs.append(o.view(c, N, -1))
+            _, pl, ds = e.decode(N, L, _copies(sh, c), present[c0:c0 + c].reshape(c * N, N).contiguous(),
+                                 root_p[c0:c0 + c].reshape(c * N, 32).contiguous(),
+                                 out=out[c0:c0 + c].view(c * N, OS))
             plens.append(pl.view(c, N))
             dsts.append(ds.view(c, N))
-        out, plen, dst = torch.cat(outs), torch.cat(plens), torch.cat(dsts)          # [v][p]...
+        plen, dst = torch.cat(plens), torch.cat(dsts)          # [v][p]
         work["decodes"] = nv * N
         out = out[..., :C] if out.shape[-1] >= C else torch.nn.functional.pad(out, (0, C - out.shape[-1]))
         le = (out[..., 48:56].to(torch.int64) << (8 * torch.arange(8, device=dev))).sum(-1)

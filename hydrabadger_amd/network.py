@@ -156,11 +156,15 @@ class DeviceEngine:
                                                   n_inst * n_nodes, flags), "Proof::validate")
         return ok.view(n_inst, n_nodes)
 
-    def decode(self, n_nodes: int, L: int, shards, present, roots):
+    def decode(self, n_nodes: int, L: int, shards, present, roots, out=None):
+        """out: optional [n_inst][OS] zeroed rows to decode into (a slice of a
+        larger table: no concatenation copy afterwards)."""
         n_inst = shards.shape[0]
         D, _ = bc.shard_counts(n_nodes)
         OS = (D * L + 15) // 16 * 16
-        out = self.zeros((n_inst, OS))
+        if out is None:
+            out = self.zeros((n_inst, OS))
+        assert out.shape == (n_inst, OS) and out.is_contiguous()
         plen = torch.zeros(n_inst, dtype=torch.int64, device=self.device)
         st = self.zeros((n_inst,))
         bc.rbc_decode_batch(n_nodes, L, shards, present, roots, out, plen, st, ctx=self.ctx, device=True,

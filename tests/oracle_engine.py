@@ -108,7 +108,7 @@ class OracleEngine:
             ok[q] = pr.validate(N)
         return torch.from_numpy(ok)
 
-    def decode(self, N, L, shards, present, roots):
+    def decode(self, N, L, shards, present, roots, out=None):
         outs, lens, st = [], [], []
         for i in range(shards.shape[0]):
             r = None
@@ -121,7 +121,12 @@ class OracleEngine:
         buf = np.zeros((len(outs), w), np.uint8)
         for i, o in enumerate(outs):
             buf[i, :len(o)] = np.frombuffer(o, np.uint8)
-        return torch.from_numpy(buf), torch.tensor(lens), torch.tensor(st, dtype=torch.uint8)
+        if out is not None:  # the engine's in-place form (rows of a larger table)
+            out[:, :w] = torch.from_numpy(buf)
+            buf = out
+        else:
+            buf = torch.from_numpy(buf)
+        return buf, torch.tensor(lens), torch.tensor(st, dtype=torch.uint8)
 
     def decrypt_shares(self, U48, sk32, pair_ct, pair_sk):
         Us = [B.g1_decompress(_b(u)) for u in U48]
