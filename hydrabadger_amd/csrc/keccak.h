@@ -154,17 +154,25 @@ __device__ __forceinline__ void sha3_256_aligned8(const uint8_t* __restrict__ p,
     keccak_zero(a);
     const uint64_t nfull = len / 136;
     const uint2* q = reinterpret_cast<const uint2*>(p);
-    for (uint64_t blk = 0; blk < nfull; ++blk) {
-        uint2 w[17];
+    // the next block's loads are issued before this block's permutation, so
+    // their latency hides under it (few waves per SIMD: configs[1]'s 2.4)
+    uint2 w[17];
+    if (nfull) {
 #pragma unroll
         for (int i = 0; i < 17; ++i) w[i] = q[i];
+    }
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
 #pragma unroll
         for (int i = 0; i < 17; ++i) {
             a[i].lo ^= w[i].x;
             a[i].hi ^= w[i].y;
         }
-        perm<IMPL>(a);
         q += 17;
+        if (blk + 1 < nfull) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w[i] = q[i];
+        }
+        perm<IMPL>(a);
     }
     // final (possibly empty) block with FIPS-202 SHA3 padding
     const uint32_t rem = (uint32_t)(len - nfull * 136);

@@ -226,20 +226,27 @@ __device__ __forceinline__ void sha3_long(const uint8_t* p, uint64_t len, uint8_
     keccak_zero(a);
     const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
     const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
-    uint64_t pos = 0;
-    for (; pos + 136 <= len; pos += 136) {
-        const uint32_t* qb = q + pos / 4;
-        uint32_t w[35];
+    // the next block's loads are issued before this block's permutation (one
+    // lane per message at one wave per SIMD: nothing else hides their latency)
+    const uint64_t nfull = len / 136;
+    uint32_t nw[35];
+    auto load = [&](uint64_t blk) {
+        const uint32_t* qb = q + blk * 34;
 #pragma unroll
-        for (int j = 0; j < 34; ++j) w[j] = qb[j];
-        w[34] = sh ? qb[34] : 0u;
+        for (int j = 0; j < 34; ++j) nw[j] = qb[j];
+        nw[34] = sh ? qb[34] : 0u;
+    };
+    if (nfull) load(0);
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
 #pragma unroll
         for (int i = 0; i < 17; ++i) {
-            a[i].lo ^= __builtin_amdgcn_alignbyte(w[2 * i + 1], w[2 * i], sh);
-            a[i].hi ^= __builtin_amdgcn_alignbyte(w[2 * i + 2], w[2 * i + 1], sh);
+            a[i].lo ^= __builtin_amdgcn_alignbyte(nw[2 * i + 1], nw[2 * i], sh);
+            a[i].hi ^= __builtin_amdgcn_alignbyte(nw[2 * i + 2], nw[2 * i + 1], sh);
         }
+        if (blk + 1 < nfull) load(blk + 1);
         perm<1>(a);
     }
+    const uint64_t pos = nfull * 136;
     const uint32_t rem = (uint32_t)(len - pos);  // < 136 bytes + FIPS-202 padding
     uint32_t w[34];
 #pragma unroll
