@@ -146,29 +146,33 @@ __device__ __forceinline__ void sha3_pair(const uint32_t (&l)[8], const uint32_t
 // SHA3-256 of `len` bytes at an 8-byte-aligned device address.  Reads only
 // bytes [0, round_up(len, 8)) — callers guarantee that range is mapped.
 // All lanes of a wave should pass the same `len` (the block loop is then
-// wave-uniform); `p` may differ per lane.
-template <int IMPL = 0>
+// wave-uniform); `p` may differ per lane.  PREFETCH: the next block's loads
+// go out before this block's permutation (+31 VGPRs: merkle_build 19.8 vs
+// 21.4 ms at N = 64; merkle_validate, at 4 -> 3 waves per SIMD, 6 % slower).
+template <int IMPL = 0, bool PREFETCH = false>
 __device__ __forceinline__ void sha3_256_aligned8(const uint8_t* __restrict__ p, uint64_t len,
                                                   uint32_t (&out)[8]) {
     u64p a[25];
     keccak_zero(a);
     const uint64_t nfull = len / 136;
     const uint2* q = reinterpret_cast<const uint2*>(p);
-    // the next block's loads are issued before this block's permutation, so
-    // their latency hides under it (few waves per SIMD: configs[1]'s 2.4)
     uint2 w[17];
-    if (nfull) {
+    if (PREFETCH && nfull) {
 #pragma unroll
         for (int i = 0; i < 17; ++i) w[i] = q[i];
     }
     for (uint64_t blk = 0; blk < nfull; ++blk) {
+        if (!PREFETCH) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w[i] = q[i];
+        }
 #pragma unroll
         for (int i = 0; i < 17; ++i) {
             a[i].lo ^= w[i].x;
             a[i].hi ^= w[i].y;
         }
         q += 17;
-        if (blk + 1 < nfull) {
+        if (PREFETCH && blk + 1 < nfull) {
 #pragma unroll
             for (int i = 0; i < 17; ++i) w[i] = q[i];
         }

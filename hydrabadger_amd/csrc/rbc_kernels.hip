@@ -545,7 +545,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
     uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)nodes * 32);
     if (live && leaf < N) {
         uint32_t d[8];
-        sha3_256_aligned8<1>(shards + (inst * N + leaf) * S, L, d);
+        sha3_256_aligned8<1, true>(shards + (inst * N + leaf) * S, L, d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) tree[leaf * 8 + i] = d[i];
         gout[2 * leaf] = make_uint4(d[0], d[1], d[2], d[3]);
