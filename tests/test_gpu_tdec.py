@@ -355,12 +355,13 @@ def test_g1_mul_u64_and_add():
             assert (from_limbs(o[:12]), from_limbs(o[12:24])) == r and o[24] == 0
 
 
-@pytest.mark.parametrize("t", [0, 5, 21, 31, 40, 42, 63, 70])
+@pytest.mark.parametrize("t", [0, 5, 21, 31, 32, 40, 42, 63, 70])
 def test_combine_kernels_interpolate_arbitrary_points(t):
     """hbg_tdec_combine over arbitrary G1 points (interpolation does not care
-    whether shares are valid): t + 1 <= 32 runs the 32-lane-group kernel,
-    t + 1 <= 64 (40, 42 = configs[4]'s t, 63) the 64-lane one, t = 70 the
-    one-lane-per-ciphertext kernel.  Shuffled sparse indices, identity
+    whether shares are valid): t + 1 <= 24 runs the 16-lane-group kernel,
+    t + 1 <= 32 the 32-lane one, t + 1 <= 64 (32: one share in the second
+    row; 40, 42 = configs[4]'s t; 63) the 32-lane one with two shares a lane,
+    t = 70 the one-lane-per-ciphertext kernel.  Shuffled sparse indices, identity
     shares, an odd ciphertext count (half-live last group), and per-ciphertext
     DuplicateEntry / undecodable-share statuses in the same call."""
     from hydrabadger_amd import _lib
