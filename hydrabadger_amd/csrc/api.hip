@@ -691,9 +691,11 @@ struct CtTable {
 
 // Ciphertexts up to which H's sponge + lines (one lane per ciphertext, one
 // wave per SIMD) and W's lines run as one grid on the aux stream beside the
-// share leaves: both fit one wave round on half of the 1,024 SIMDs (the
-// configs[4] epoch's 16,384 ciphertexts per call).
-constexpr uint32_t kLinesBesideLeavesMax = 32768;
+// share leaves.  The configs[4] epoch's 16,384 ciphertexts per call fit one
+// wave round on half of the 1,024 SIMDs (the leaves take the rest: 584 ->
+// 516 ms per epoch); at configs[3]'s 100 k the grid's tail rounds share the
+// chip with the leaves instead of idling (826-831 -> 819-822 ms, r05o).
+constexpr uint32_t kLinesBesideLeavesMax = 131072;
 constexpr uint32_t kLinesBesideLeavesMin = 8193;  // fewer: the wave sponge (v_digest, <= 8,192) and H on this stream
 
 // W's decode (the final status) and lines on the aux stream; H = hash_g1_g2(U, V)
