@@ -1129,10 +1129,29 @@ def main():
             "leg_errors": run_leg.errors or None,
             "distributed": dist_info(dist),
         }
+        line["checks_final"] = checks_final(line)  # last key: survives a driver that keeps the line's tail
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist:
         torch.distributed.destroy_process_group()
+    if rank == 0:
+        sys.exit(exit_status(line))
+
+
+def checks_final(line: dict) -> dict:
+    """The compact verdicts repeated as the line's LAST key: every check
+    that ran (None = the leg did not run), the failed legs' names, all_ok."""
+    c = {k: v for k, v in line["checks"].items() if v is not None and k != "all_ok"}
+    c["leg_errors"] = sorted(line.get("leg_errors") or {})
+    c["all_ok"] = all(bool(v) for k, v in c.items() if k != "leg_errors") and not c["leg_errors"]
+    return c
+
+
+def exit_status(line: dict) -> int:
+    """0 only when every check that ran is true and no leg failed: a wrong
+    result or a crashed leg makes the run fail loudly (the line is still
+    printed first)."""
+    return 0 if line["checks_final"]["all_ok"] else 1
 
 
 if __name__ == "__main__":

@@ -52,6 +52,12 @@ HBG_ASYNC = 2
 HBG_DECODE_OK = 1
 HBG_DECODE_NONE = 0
 
+# hbg_set_share_verify: the batched small-exponent test (default; a 1 bit is
+# the crate's except with probability <= 2^-127) or the crate's per-share
+# equation for every share (deterministic)
+HBG_VERIFY_BATCHED = 0
+HBG_VERIFY_PER_SHARE = 1
+
 # (name, restype, argtypes) for every symbol include/hbgpu.h declares.
 _vp, _u8p, _u32, _u64, _i = C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
 SIGNATURES = {
@@ -83,6 +89,7 @@ SIGNATURES = {
     "hbg_wire_sign_frames": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _u8p, _vp, _u32]),
     "hbg_wire_verify_frames": (_i, [_vp, _u32, _u8p, _u64, _vp, _u8p, _vp, _vp, _u32]),
     "hbg_synth_bytes": (_i, [_vp, _u32, _u64, _u64, _u8p, _u64, _u64, _u32]),
+    "hbg_set_share_verify": (_i, [_vp, C.c_int]),
     "hbg_tdec_verify_shares": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u32, _u8p, _u64, _u8p, _vp, _vp, _u8p, _u32]),
     "hbg_ct_verify": (_i, [_vp, _u32, _u8p, _u8p, _vp, _u8p, _u8p, _u32]),
     "hbg_tdec_combine": (_i, [_vp, _u32, _u32, _u8p, _vp, _u8p, _vp, _u8p, _vp, _u32]),
@@ -173,6 +180,11 @@ class Context:
 
     def sync(self) -> None:
         check(lib().hbg_sync(self.h), "hbg_sync")
+
+    def set_share_verify(self, mode: int) -> None:
+        """HBG_VERIFY_BATCHED (default) or HBG_VERIFY_PER_SHARE (every
+        share-validity bit from the crate's own per-share equation)."""
+        check(lib().hbg_set_share_verify(self.h, mode), "hbg_set_share_verify")
 
 
 _default: Context | None = None

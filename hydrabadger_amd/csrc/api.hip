@@ -6,9 +6,11 @@
 // calls (HBG_DEVICE) run in place on the caller's buffers.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/random.h>
 
 #include <initializer_list>
 #include <map>
@@ -48,6 +50,12 @@ struct hbg_ctx {
     // rounds); 2 batched + pk tables always (and, for signature shares, no speculative 16-group round);
     // 3 batched at every size.  pk fixed-base tables when each key verifies >= kPkTableMinUses shares.
     int tdec_batched = 1;
+    // hbg_set_share_verify: HBG_VERIFY_PER_SHARE pins every share-validity bit to
+    // one independent pairing check per share (the reference's deterministic
+    // equation) whatever the size; it overrides the test hook above
+    int verify_mode = HBG_VERIFY_BATCHED;
+    // secret key of the batched verifier's weights (getrandom at hbg_init; never exposed)
+    bls::BatchKey batch_key{};
     // hbg_rbc_encode_merkle schedule (hbg_test_set_rbc_fused): 0 rs_encode_const + merkle_build, 1 the
     // fused rbc_encode_merkle, -1 (default) fused where it measured faster: (D, Q) = (22, 42), N = 64
     int rbc_fused = -1;
@@ -212,6 +220,21 @@ int device_encode_plan(hbg_ctx* c, uint32_t D, uint32_t Q, uint8_t** out) {
 
 bool aligned(const void* p, uintptr_t a) { return ((uintptr_t)p % a) == 0; }
 
+// Kernel CSPRNG bytes (getrandom(2), blocking until the pool is initialised).
+bool fill_random(void* out, size_t n) {
+    uint8_t* p = (uint8_t*)out;
+    while (n) {
+        const ssize_t r = getrandom(p, n, 0);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        p += r;
+        n -= (size_t)r;
+    }
+    return true;
+}
+
 // Synchronise the context stream and return (and clear) the first error a
 // kernel flagged since the last such point (dev_err.h).
 int sync_status(hbg_ctx* c) {
@@ -350,6 +373,11 @@ int hbg_init(hbg_ctx** out, int device) {
         return HBG_E_DEVICE;
     }
     c->stream = c->own;
+    if (!fill_random(c->batch_key.w, sizeof(c->batch_key.w))) {  // no batch weights without a secret
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return HBG_E_DEVICE;
+    }
     if (hipMalloc(&c->d_err, sizeof(int32_t)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int32_t)) != hipSuccess) {
         (void)hipStreamDestroy(c->own);
         delete c;
@@ -810,6 +838,7 @@ constexpr uint64_t kPkTableMinUses = 2048;
 // 1,024 SIMDs x 2 waves x 64 lanes (measured crossover).
 constexpr uint64_t kBatchMinShares = 3ull * 1024 * 2 * 64;
 bool use_batched(const hbg_ctx* c, uint64_t n) {
+    if (c->verify_mode == HBG_VERIFY_PER_SHARE) return false;
     if (c->tdec_batched == 0 || n < 2 || n >= (1ull << 31)) return false;
     return c->tdec_batched >= 2 || n >= kBatchMinShares;
 }
@@ -910,7 +939,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, CtTable& t, const uint8_t* 
     }
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
     HBG_TRY(bls::launch_tdec_batch_leaves(nb, counts + 3, n_ct, ds, pm, dsh, dsp, dU48, t.u_status, paff, pst, tbl,
-                                          (uint32_t*)sums, (uint8_t*)lok, c->stream, share_aff));
+                                          (uint32_t*)sums, (uint8_t*)lok, c->batch_key, c->stream, share_aff));
     HBG_DBG_STEP(c, "batch_leaves");
     HBG_CHECK(wait_lines(c));  // the line tables (launch_lines: beside the leaves)
     if (after_leaves) HBG_CHECK(after_leaves());
@@ -1196,7 +1225,8 @@ int hbg_tdec_threshold_decrypt(hbg_ctx* c, uint32_t t, uint32_t n_nodes, uint32_
     HBG_CHECK(scratch(c, 39, 4ull * (32 * m > 36 ? 32 * m : 36) * n_ct, &scr));
     HBG_CHECK(scratch(c, 41, 32ull * n_ct, &sds));
     HBG_TRY(bls::launch_tdec_combine(n_ct, t, s48, sidx, dV, dVoff, (uint8_t*)dpt, (int32_t*)dst, (uint32_t*)scr,
-                                     (uint8_t*)sds, c->stream, (const uint32_t*)saff, n_nodes, sst));
+                                     (uint8_t*)sds, c->stream, (const uint32_t*)saff, n_nodes, sst,
+                                     (const uint8_t*)okb));
     HBG_TRY(bls::launch_tdec_status_merge(n_ct, sst, (int32_t*)dst, c->stream));
     return drain(c, flags, {{plaintext, {dpt, vlen}}, {status, {dst, 4ull * n_ct}}, {outcome, {doc, n}}});
 }
@@ -1414,7 +1444,7 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
                                         (uint32_t*)tb, (bls::BatchDesc*)desc, temp, tb_bytes, counts + 3, c->stream));
     HBG_TRY(hipMemsetAsync(o, 0, n, c->stream));
     HBG_TRY(bls::launch_sig_batch_leaves(nb, counts + 3, n_doc, ds, pm, sh, sp, (const uint8_t*)seeds, pa, ps, tbl,
-                                         (uint32_t*)sums, (uint8_t*)lok, c->stream));
+                                         (uint32_t*)sums, (uint8_t*)lok, c->batch_key, c->stream));
     // Check rounds run one pairing per lane and are latency-bound below ~1 wave
     // per SIMD; while 5 items per batch still fit one such wave per SIMD, the
     // 16-groups are checked speculatively in round 0 (one round fewer).  The
@@ -1440,6 +1470,13 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
     HBG_TRY(bls::launch_sig_verify_shares(n, counts + 1, (const uint32_t*)fails, sh, sd, sp, pa, ps, ch, ln, o,
                                           c->stream));
     return drain(c, flags, {{ok, {dok, n}}});
+}
+
+int hbg_set_share_verify(hbg_ctx* c, int mode) {
+    if (!c || (mode != HBG_VERIFY_BATCHED && mode != HBG_VERIFY_PER_SHARE)) return HBG_E_ARG;
+    CtxLock g(c);
+    c->verify_mode = mode;
+    return HBG_OK;
 }
 
 int hbg_test_set_tdec_batched(hbg_ctx* c, int on) {

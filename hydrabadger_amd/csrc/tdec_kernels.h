@@ -14,6 +14,12 @@ constexpr uint32_t kBatchShares = 64;             // batched verification: share
 
 struct BatchDesc;
 struct CheckItem;
+// Secret key of the batch weights: 32 bytes drawn from getrandom(2) once per
+// context (hbg_init) and never exposed, so a sender cannot predict the weight
+// its share gets, nor grind shares offline against them.
+struct BatchKey {
+    uint32_t w[8];
+};
 constexpr uint32_t kBatchDescBytes = 16, kCheckItemBytes = 8, kBinItemBytes = 16;
 constexpr uint32_t kBatchSumBytes = 64 * 2 * 36 * 4;  // per batch: the binary tree's root + left nodes (2 G1 sums each)
 constexpr uint32_t kGtBytes = 144 * 4;                // a GT value (Fp12)
@@ -65,7 +71,8 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
                                     const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
-                                    uint8_t* leaf_ok, hipStream_t st, uint32_t* share_aff = nullptr);
+                                    uint8_t* leaf_ok, const BatchKey& key, hipStream_t st,
+                                    uint32_t* share_aff = nullptr);
 size_t tdec_pk_table_bytes(uint32_t n_pk);
 hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st);
 // Binary group testing (tdec_kernels.hip "batched share verification"):
@@ -106,7 +113,8 @@ hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t
 hipError_t launch_sig_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_doc, const BatchDesc* desc,
                                    const uint32_t* perm, const uint8_t* share96, const uint32_t* share_pk,
                                    const uint8_t* seeds, const uint32_t* pk_aff, const int32_t* pk_status,
-                                   const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, hipStream_t st);
+                                   const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, const BatchKey& key,
+                                   hipStream_t st);
 hipError_t launch_sig_batch_check(uint32_t cap, const uint32_t* n_dev, uint32_t spec, const CheckItem* items,
                                   const BatchDesc* desc, const uint32_t* perm, const uint32_t* sums,
                                   const uint8_t* leaf_ok, const uint32_t* coefH, uint32_t* lines, uint8_t* ok,
@@ -129,11 +137,15 @@ hipError_t launch_tdec_status_merge(uint32_t n, const int32_t* sel_status, int32
 // written by the share verification (leaves / verify_shares): the combine
 // reads share idx[i] of ciphertext g there instead of decompressing share48;
 // pre_status (nullable, with share_aff): a ciphertext whose selection failed
-// is skipped (its status is the selection's).
+// is skipped (its status is the selection's); share_ok (nullable, with
+// share_aff): the verification's bits [n][n_nodes] — a selected share whose
+// bit is 0 (a validator's own share, inserted unverified) has no share_aff
+// entry and is decompressed from share48 (undecodable: HBG_E_INVALID_POINT).
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff = nullptr,
-                               uint32_t n_nodes = 0, const int32_t* pre_status = nullptr);
+                               uint32_t n_nodes = 0, const int32_t* pre_status = nullptr,
+                               const uint8_t* share_ok = nullptr);
 hipError_t launch_tdec_test(int op, uint32_t n, const uint32_t* in, uint32_t* out, uint32_t in_words,
                             uint32_t out_words, uint32_t* lines, hipStream_t st);
 

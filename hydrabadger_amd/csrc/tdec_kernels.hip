@@ -1126,9 +1126,16 @@ __global__ __launch_bounds__(256) void tdec_index_sanitize(uint64_t n, const uin
 // ---------------------------------------------------------------- batched share verification
 // verify_decryption_share for many shares of ONE ciphertext c shares (H, W):
 // e(S_i, H) == e(PK_i, W) for all i in a batch  <=  e(sum r_i S_i, H) ==
-// e(sum r_i PK_i, W) with 64-bit weights r_i derived from a digest of the
-// whole batch (Bellare-Garay-Rabin small-exponent batch test; a batch holding
-// an invalid share passes with probability <= 2^-63).  A batch is up to 64
+// e(sum r_i PK_i, W) with secret 127-bit weights r_i (Bellare-Garay-Rabin
+// small-exponent batch test).  r_i = a_i + b_i x^2 with a_i (odd) and b_i the
+// two 64-bit halves of SHA3(K || D || i): K is the context's secret batch key
+// (32 bytes from getrandom at hbg_init, never exposed), D a digest of the whole
+// batch.  The 2^127 (a, b) pairs are 2^127 distinct integers below the group
+// order (a < 2^64 < x^2; r < 2^193), so for any batch holding an invalid share
+// and any fixed choice of the other weights at most one value of r_i makes the
+// weighted product 1: a (sub)tree holding an invalid share passes with
+// probability <= 2^-127, and no sender can grind shares against the weights
+// offline (without K they are unpredictable).  A batch is up to 64
 // shares of one ciphertext, tested as a BINARY tree with sibling derivation
 // (round 5): round 0 checks every batch sum; a failing node's left child is
 // checked and its right child's value is DERIVED — the checks are values in
@@ -1137,9 +1144,9 @@ __global__ __launch_bounds__(256) void tdec_index_sanitize(uint64_t n, const uin
 // in the cyclotomic subgroup is the conjugate).  Each failing node costs one
 // pairing, and six rounds (32, 16, 8, 4, 2, 1 shares) reach the single
 // shares.  A single's value is g^r for g = e(S, H) e(-PK, W) and its weight r
-// (a + b x^2 with a odd, < 2^161 < the group order: never 0 mod r), so it is
-// 1 exactly when the reference's per-share equation holds: every reported 0
-// is that equation's verdict, every 1 a passing (sub)tree's.  Round 4's 4-ary
+// (nonzero and below the group order), so it is 1 exactly when the
+// reference's per-share equation holds: every reported 0 is that equation's
+// verdict, every 1 a passing (sub)tree's.  Round 4's 4-ary
 // tree (4 checks per failing node, three rounds) ran its rounds at 2-4 full
 // generations of one wave per SIMD; here a round holds ~one check per bad
 // share (<= 64 k items at 1 % of 6.4 M: one generation).
@@ -1220,14 +1227,14 @@ BD G1 g1_shfl_xor(const G1& p, int m) {
 
 // Fixed-base tables of the public key shares for the batch weights:
 // tbl[pk][w][v] = affine [v * 2^(8w)] PK_pk, v in 1..255, w in 0..7 (v = 0
-// unused), so [r] PK for a 64-bit weight is 8 mixed additions, no doublings.
+// unused), so [a] PK for a 64-bit weight half is 8 mixed additions, no
+// doublings (the b half reads the same entries through (beta x, -y)).
 constexpr uint32_t kPkTblWords = 8 * 256 * 24;
 TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
                                                     uint32_t* __restrict__ tbl) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // (pk, w, v)
     if (i >= n_pk * 2048u) return;
     const uint32_t pk = i >> 11, w = (i >> 8) & 7u, v = i & 255u;
-    if (w >= 4) return;  // batch weights use 32-bit halves: windows 0..3
     const uint32_t* pa = pk_aff + 32ull * pk;
     uint32_t* o = tbl + (uint64_t)pk * kPkTblWords + (uint64_t)(w * 256 + v) * 24;
     if (v == 0 || pa[24] != 0) return;
@@ -1240,10 +1247,10 @@ TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_af
 // weight, and the quad / 16-group / batch sums by cross-lane butterfly
 // (ds_swizzle/bpermute shuffles: no LDS for the points, so occupancy is set
 // by VGPRs alone).
-// [a]P + [b]([x^2]P) for P in G1 (affine) and 32-bit a, b: on G1 [x^2]P =
+// [a]P + [b]([x^2]P) for P in G1 (affine) and 64-bit a, b: on G1 [x^2]P =
 // -phi(P) = (beta px, -py), so the batch weight r = a + b x^2 (mod r; the
-// 2^64 pairs give 2^64 distinct weights) costs a 32-bit joint double-and-add
-// (branch-free addend select, as g1_mul_fr) instead of a 64-bit one.
+// 2^128 pairs give 2^128 distinct weights) costs a 64-bit joint double-and-add
+// (branch-free addend select, as g1_mul_fr) instead of a 128-bit one.
 // The three addends P, [x^2]P and both = P + [x^2]P = (X, Y, Z) share one
 // denominator on the isomorphic curve E_Z: y^2 = x^3 + 4 Z^6, reached by
 // (x, y) -> (x Z^2, y Z^3): there both is the affine (X, Y) and P, [x^2]P are
@@ -1252,7 +1259,7 @@ TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_af
 // with mixed additions (11 multiplications instead of 16) and the result
 // (X', Y', Z') maps back to E as (X', Y', Z' Z).  Z != 0: (1 + x^2) P != O
 // for P in G1.
-BD G1 g1_mul_ab32(const Fp& px, const Fp& py, uint32_t a, uint32_t b) {
+BD G1 g1_mul_ab64(const Fp& px, const Fp& py, uint64_t a, uint64_t b) {
     const G1 both = g1_add_mixed({px, py, fp_one()}, fp_mul(px, fp_const(kBeta)), fp_neg(py));
     Fp z2 = fp_sqr(both.z), z3, tx, ty;
     z3 = fp_mul(z2, both.z);
@@ -1260,13 +1267,50 @@ BD G1 g1_mul_ab32(const Fp& px, const Fp& py, uint32_t a, uint32_t b) {
     const Fp ux = fp_mul(tx, fp_const(kBeta)), uy = fp_neg(ty);
     G1 r = {fp_one(), fp_one(), fp_zero()};
 #pragma unroll 1
-    for (int bit = 31; bit >= 0; --bit) {
+    for (int bit = 63; bit >= 0; --bit) {
         r = g1_dbl(r);
         const bool ea = (a >> bit) & 1u, eb = (b >> bit) & 1u;
         const G1 sum = g1_add_mixed(r, ea ? (eb ? both.x : tx) : ux, ea ? (eb ? both.y : ty) : uy);
         if (ea || eb) r = sum;
     }
     return {r.x, r.y, fp_mul(r.z, both.z)};
+}
+
+// The batch weight of lane i: (a, b) = the two 64-bit halves of
+// SHA3(K || D || i) (K: the context's secret batch key, D: the batch digest),
+// a forced odd so r = a + b x^2 is never 0.
+BD void batch_weight(const BatchKey& key, const uint8_t* D, uint32_t lane, uint64_t& a, uint64_t& b) {
+    uint8_t m[68], dg[32];
+    for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 4; ++j) m[4 * i + j] = (uint8_t)(key.w[i] >> (8 * j));
+    for (int i = 0; i < 32; ++i) m[32 + i] = D[i];
+    for (int i = 0; i < 4; ++i) m[64 + i] = (uint8_t)(lane >> (8 * i));
+    sha3_bytes(m, 68, dg);
+    a = 0;
+    b = 0;
+    for (int i = 0; i < 8; ++i) {
+        a |= (uint64_t)dg[i] << (8 * i);
+        b |= (uint64_t)dg[8 + i] << (8 * i);
+    }
+    a |= 1u;
+}
+
+// [a + b x^2] PK from the key's fixed-base table (windows 0..7 of both halves;
+// the b half through (beta x, -y)): 16 mixed additions, no doublings.
+BD G1 pk_tbl_mul_ab64(const uint32_t* t, uint64_t a, uint64_t b) {
+    G1 B = {fp_one(), fp_one(), fp_zero()};
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t va = (uint32_t)(a >> (8 * w)) & 255u, vb = (uint32_t)(b >> (8 * w)) & 255u;
+        if (va) {
+            const uint32_t* e = t + (w * 256 + va) * 24;
+            B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+        }
+        if (vb) {
+            const uint32_t* e = t + (w * 256 + vb) * 24;
+            B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
+        }
+    }
+    return B;
 }
 
 TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb_dev, uint32_t n_ct,
@@ -1280,7 +1324,7 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
                                                         const int32_t* __restrict__ pk_status,
                                                         const uint32_t* __restrict__ pk_tbl,
                                                         uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok,
-                                                        uint32_t* __restrict__ share_aff) {
+                                                        const BatchKey key, uint32_t* __restrict__ share_aff) {
     // ct_status: U's decode status (the ciphertext table's final status, W's
     // decode included, is applied by the root round)
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
@@ -1301,10 +1345,9 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
     G1A s;
     if (valid) valid = g1_decompress(share48 + 48ull * k, s, true);
     if (valid && share_aff) store_aff(share_aff + (uint64_t)kAffWords * k, s);  // for the combine
-    // Weights are bound to the WHOLE batch (Fiat-Shamir): leaf digest
-    // d_i = SHA3(U || S_i || pk_i), batch digest D = SHA3(d_0 || ... ),
-    // r_i = SHA3(D || i)[0..8] | 1 — changing any share re-randomises every
-    // weight, so shares cannot be ground against each other's weights.
+    // Weights: r_i from SHA3(K || D || i) with D = SHA3(d_0 || ...) over the
+    // leaf digests d_i = SHA3(U || S_i || pk_i) — secret (K) and bound to the
+    // whole batch (changing any share re-randomises every weight).
     if (in && real_ct) {
         uint8_t m[100];
         for (int i = 0; i < 48; ++i) m[i] = U48[48ull * d.ct + i];
@@ -1317,38 +1360,15 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
     __syncthreads();
     G1 A = {fp_one(), fp_one(), fp_zero()}, B = A;
     if (valid) {
-        uint8_t m[36], dg[32];
-        for (int i = 0; i < 32; ++i) m[i] = sBatch[i];
-        for (int i = 0; i < 4; ++i) m[32 + i] = (uint8_t)(lane >> (8 * i));
-        sha3_bytes(m, 36, dg);
         // weight r_i = a + b x^2 (a odd: nonzero); S_i and pk_i are in G1
         // (decoded with the subgroup check), where [x^2]P = (beta px, -py)
-        uint32_t ra = 0, rb = 0;
-        for (int i = 0; i < 4; ++i) {
-            ra |= (uint32_t)dg[i] << (8 * i);
-            rb |= (uint32_t)dg[4 + i] << (8 * i);
-        }
-        ra |= 1u;
-        if (!s.inf) A = g1_mul_ab32(s.x, s.y, ra, rb);
+        uint64_t ra, rb;
+        batch_weight(key, sBatch, lane, ra, rb);
+        if (!s.inf) A = g1_mul_ab64(s.x, s.y, ra, rb);
         const uint32_t* pa = pk_aff + 32ull * pk;
-        if (pa[24] == 0) {
-            if (pk_tbl) {  // windows 0..3 of the [v 256^w]pk table; the b half through (beta x, -y)
-                const uint32_t* t = pk_tbl + (uint64_t)pk * kPkTblWords;
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t va = (ra >> (8 * w)) & 255u, vb = (rb >> (8 * w)) & 255u;
-                    if (va) {
-                        const uint32_t* e = t + (w * 256 + va) * 24;
-                        B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
-                    }
-                    if (vb) {
-                        const uint32_t* e = t + (w * 256 + vb) * 24;
-                        B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
-                    }
-                }
-            } else {
-                B = g1_mul_ab32(load_fp(pa), load_fp(pa + 12), ra, rb);
-            }
-        }
+        if (pa[24] == 0)
+            B = pk_tbl ? pk_tbl_mul_ab64(pk_tbl + (uint64_t)pk * kPkTblWords, ra, rb)
+                       : g1_mul_ab64(load_fp(pa), load_fp(pa + 12), ra, rb);
     }
     leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
     // the binary tree's left nodes (slot h / 2) and the root (slot 0): the
@@ -1901,7 +1921,7 @@ BD G1 g1_mul_fr(const Fp& px, const Fp& py, const uint32_t (&l)[8]) {
     uint32_t q[5], rm[5];
     split_x2(l, q, rm);
     // P + [x^2]P (never infinity) and the addends on its isomorphic curve E_Z
-    // (g1_mul_ab32): mixed additions only, the result mapped back by Z
+    // (g1_mul_ab64): mixed additions only, the result mapped back by Z
     const G1 both = g1_add_mixed({px, py, fp_one()}, fp_mul(px, fp_const(kBeta)), fp_neg(py));
     Fp z2 = fp_sqr(both.z), z3, tx, ty;
     z3 = fp_mul(z2, both.z);
@@ -1946,7 +1966,8 @@ template <int G, int MMAX>
 TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restrict__ share48,
                                   const uint32_t* __restrict__ idx, uint32_t* __restrict__ sums,
                                   int32_t* __restrict__ status, const uint32_t* __restrict__ share_aff,
-                                  uint32_t n_nodes, const int32_t* __restrict__ pre_status) {
+                                  uint32_t n_nodes, const int32_t* __restrict__ pre_status,
+                                  const uint8_t* __restrict__ share_ok) {
     static_assert(G == 16 || G == 32 || G == 64, "a quarter, half or whole wave per ciphertext");
     static_assert(MMAX <= 2 * G, "at most two shares per lane");
     constexpr uint32_t GPB = 64 / G;                 // groups per 64-lane block
@@ -1978,9 +1999,12 @@ TDEC_KERNEL void tdec_combine_msm(uint32_t n, uint32_t t, const uint8_t* __restr
         if (act)
             for (uint32_t j = sI + 1; j < m; ++j) dup |= ix[j] == me[r];
         if (act && pre == 0) {
-            if (share_aff) {  // the verification's decoded point (a selected share is a verified one)
-                const uint32_t* a =
-                    share_aff + ((uint64_t)g * n_nodes + (me[r] < n_nodes ? me[r] : 0u)) * kAffWords;
+            const uint64_t slot = (uint64_t)g * n_nodes + (me[r] < n_nodes ? me[r] : 0u);
+            // the verification's decoded point for a selected share that verified;
+            // a selected share that did not (a validator's own share: trusted, never
+            // verified — it may not even decode) is decompressed here
+            if (share_aff && (!share_ok || share_ok[slot])) {
+                const uint32_t* a = share_aff + slot * kAffWords;
                 p[r].x = load_fp(a);
                 p[r].y = load_fp(a + 12);
                 p[r].inf = a[24] != 0;
@@ -2127,7 +2151,7 @@ BD G2 g2_mul_scalar(const Fp2& px, const Fp2& py, const uint32_t (&k)[8]) {
     split_x2(k, q, rm);
     const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));  // [x^2]P, Z = 1
     const G2 both = g2_add_mixed({px, py, fp2_one()}, B.x, B.y);
-    // the addends on the isomorphic curve of both's Z (g1_mul_ab32): mixed additions
+    // the addends on the isomorphic curve of both's Z (g1_mul_ab64): mixed additions
     const Fp2 z2 = fp2_sqr(both.z), z3 = fp2_mul(z2, both.z);
     const Fp2 tx = fp2_mul(px, z2), ty = fp2_mul(py, z3), ux = fp2_mul(B.x, z2), uy = fp2_mul(B.y, z3);
     G2 r = {fp2_one(), fp2_one(), fp2_zero()};
@@ -2461,10 +2485,10 @@ TDEC_WAVE1_KERNEL void coin_combine_grp(uint32_t n, uint32_t t, const uint8_t* _
 // §8(f3)) for the shares of ONE document: e(pk_i, H) == e(G1, sig_i) for all
 // i  <=  e(sum r_i pk_i, H) == e(G1, sum r_i sig_i), H = hash_g2(doc) hashed
 // and prepared ONCE per document (the per-share bls_verify hashes to G2 and
-// prepares H once per share).  Same Fiat-Shamir weights, 4-ary group-testing
-// tree and per-share fallback as the decryption shares above, so every 0 bit
-// is the reference's per-share equation and a 1 from a passing (sub)batch is
-// wrong with probability <= 2^-63.
+// prepares H once per share).  Same secret 127-bit weights (batch_weight), a
+// 4-ary group-testing tree and per-share fallback as the decryption shares
+// above, so every 0 bit is the reference's per-share equation and a 1 from a
+// passing (sub)batch is wrong with probability <= 2^-127.
 constexpr uint32_t kG2JacWords = 72;
 constexpr uint32_t kSigSumWords = kJacWords + kG2JacWords;  // (sum r pk: G1, sum r sig: G2)
 constexpr uint32_t kSigBatchSumWords = kNodes * kSigSumWords;
@@ -2494,23 +2518,23 @@ TDEC_WAVE1_KERNEL void sig_doc_prepare(uint32_t n, const uint8_t* __restrict__ d
 }
 
 // One 64-lane block per batch (shares of one document), lane = share: decode
-// the G2 share with the crate's subgroup check, weight r_i = SHA3(D || i)
-// (D = SHA3 of the leaf digests SHA3(doc seed || share || key index)), then
+// the G2 share with the crate's subgroup check, weight r_i from SHA3(K || D || i)
+// (batch_weight; D = SHA3 of the leaf digests SHA3(doc seed || share || key index)), then
 // [r_i] sig_i (G2) and [r_i] pk_i (G1, fixed-base tables when given) and the
 // quad / 16-group / batch sums by cross-lane butterflies.
-// [a]P + [b]psi^2(P) = [a + b x^2]P for P in G2 (affine), 32-bit a, b (psi = [x]
+// [a]P + [b]psi^2(P) = [a + b x^2]P for P in G2 (affine), 64-bit a, b (psi = [x]
 // on G2; psi^2 of an affine point is affine) — the G2 half of the coin
 // shares' batch weights, same joint double-and-add (and the same mixed
 // additions on the isomorphic curve y^2 = x^3 + b' Z^6 of the common
-// denominator Z of both = P + psi^2(P)) as g1_mul_ab32.
-BD G2 g2_mul_ab32(const Fp2& px, const Fp2& py, uint32_t a, uint32_t b) {
+// denominator Z of both = P + psi^2(P)) as g1_mul_ab64.
+BD G2 g2_mul_ab64(const Fp2& px, const Fp2& py, uint64_t a, uint64_t b) {
     const G2 B = g2_psi(g2_psi({px, py, fp2_one()}));  // affine: conj(conj(1)) = 1
     const G2 both = g2_add_mixed({px, py, fp2_one()}, B.x, B.y);
     const Fp2 z2 = fp2_sqr(both.z), z3 = fp2_mul(z2, both.z);
     const Fp2 tx = fp2_mul(px, z2), ty = fp2_mul(py, z3), ux = fp2_mul(B.x, z2), uy = fp2_mul(B.y, z3);
     G2 r = {fp2_one(), fp2_one(), fp2_zero()};
 #pragma unroll 1
-    for (int bit = 31; bit >= 0; --bit) {
+    for (int bit = 63; bit >= 0; --bit) {
         r = g2_dbl(r);
         const bool ea = (a >> bit) & 1u, eb = (b >> bit) & 1u;
         const G2 sum = g2_add_mixed(r, ea ? (eb ? both.x : tx) : ux, ea ? (eb ? both.y : ty) : uy);
@@ -2524,7 +2548,7 @@ TDEC_WAVE1_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict
                                   const uint8_t* __restrict__ share96, const uint32_t* __restrict__ share_pk,
                                   const uint8_t* __restrict__ seeds, const uint32_t* __restrict__ pk_aff,
                                   const int32_t* __restrict__ pk_status, const uint32_t* __restrict__ pk_tbl,
-                                  uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok) {
+                                  uint32_t* __restrict__ sums, uint8_t* __restrict__ leaf_ok, const BatchKey key) {
     __shared__ uint8_t sDig[kBatchShares * 32], sBatch[32];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     if (b >= dev_count(nb_dev, cap)) return;  // grid sized for the bound; the batch count is a device word
@@ -2546,42 +2570,17 @@ TDEC_WAVE1_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict
     __syncthreads();
     if (lane == 0) sha3_bytes(sDig, 32u * (d.end - d.start), sBatch);
     __syncthreads();
-    uint32_t ra = 0, rb = 0;  // weight r_i = a + b x^2 (a odd: nonzero); pk_i in G1, sig_i in G2
-    if (valid) {
-        uint8_t m[36], dg[32];
-        for (int i = 0; i < 32; ++i) m[i] = sBatch[i];
-        for (int i = 0; i < 4; ++i) m[32 + i] = (uint8_t)(lane >> (8 * i));
-        sha3_bytes(m, 36, dg);
-        for (int i = 0; i < 4; ++i) {
-            ra |= (uint32_t)dg[i] << (8 * i);
-            rb |= (uint32_t)dg[4 + i] << (8 * i);
-        }
-        ra |= 1u;
-    }
+    uint64_t ra = 0, rb = 0;  // weight r_i = a + b x^2 (a odd: nonzero); pk_i in G1, sig_i in G2
+    if (valid) batch_weight(key, sBatch, lane, ra, rb);
     leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
     uint32_t* out = sums + (uint64_t)b * kSigBatchSumWords;
     // G1 side: sum r_i pk_i
     {
         G1 B = {fp_one(), fp_one(), fp_zero()};
         const uint32_t* pa = pk_aff + 32ull * pk;
-        if (valid && pa[24] == 0) {
-            if (pk_tbl) {  // windows 0..3 of the [v 256^w]pk table; the b half through (beta x, -y)
-                const uint32_t* t = pk_tbl + (uint64_t)pk * kPkTblWords;
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t va = (ra >> (8 * w)) & 255u, vb = (rb >> (8 * w)) & 255u;
-                    if (va) {
-                        const uint32_t* e = t + (w * 256 + va) * 24;
-                        B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
-                    }
-                    if (vb) {
-                        const uint32_t* e = t + (w * 256 + vb) * 24;
-                        B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
-                    }
-                }
-            } else {
-                B = g1_mul_ab32(load_fp(pa), load_fp(pa + 12), ra, rb);
-            }
-        }
+        if (valid && pa[24] == 0)
+            B = pk_tbl ? pk_tbl_mul_ab64(pk_tbl + (uint64_t)pk * kPkTblWords, ra, rb)
+                       : g1_mul_ab64(load_fp(pa), load_fp(pa + 12), ra, rb);
 #pragma unroll 1
         for (int m = 1; m < 64; m <<= 1) {
             B = g1_add(B, g1_shfl_xor(B, m));
@@ -2593,7 +2592,7 @@ TDEC_WAVE1_KERNEL void sig_batch_leaves(uint32_t cap, const uint32_t* __restrict
     // G2 side: sum r_i sig_i
     {
         G2 A = {fp2_one(), fp2_one(), fp2_zero()};
-        if (valid && !s.inf) A = g2_mul_ab32(s.x, s.y, ra, rb);
+        if (valid && !s.inf) A = g2_mul_ab64(s.x, s.y, ra, rb);
 #pragma unroll 1
         for (int m = 1; m < 64; m <<= 1) {
             A = g2_add(A, g2_shfl_xor(A, m));
@@ -2788,7 +2787,7 @@ hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff,
-                               uint32_t n_nodes, const int32_t* pre_status);
+                               uint32_t n_nodes, const int32_t* pre_status, const uint8_t* share_ok);
 hipError_t launch_bls_sign(uint64_t n, uint32_t n_sk, const uint8_t* sk32, const uint32_t* msg_sk,
                            const uint8_t* msg, const uint64_t* off, uint8_t* sig96, int32_t* err, hipStream_t st);
 hipError_t launch_bls_verify(uint64_t n, uint32_t n_pk, const uint32_t* pk_aff, const int32_t* pk_status,
@@ -3021,11 +3020,11 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     const uint32_t* perm, const uint8_t* share48, const uint32_t* share_pk,
                                     const uint8_t* U48, const int32_t* ct_status, const uint32_t* pk_aff,
                                     const int32_t* pk_status, const uint32_t* pk_tbl, uint32_t* sums,
-                                    uint8_t* leaf_ok, hipStream_t st, uint32_t* share_aff) {
+                                    uint8_t* leaf_ok, const BatchKey& key, hipStream_t st, uint32_t* share_aff) {
     HBG_COUNT_MARK("tdec_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
     tdec_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_max, nb_dev, n_ct, desc, perm, share48, share_pk, U48, ct_status,
-                                                         pk_aff, pk_status, pk_tbl, sums, leaf_ok, share_aff);
+                                                         pk_aff, pk_status, pk_tbl, sums, leaf_ok, key, share_aff);
     return hipGetLastError();
 }
 
@@ -3094,23 +3093,23 @@ hipError_t launch_tdec_ct_verify(uint32_t n, const uint32_t* ct_u, const int32_t
 hipError_t launch_tdec_combine(uint32_t n, uint32_t t, const uint8_t* share48, const uint32_t* idx,
                                const uint8_t* V, const uint64_t* V_off, uint8_t* out, int32_t* status,
                                uint32_t* scratch, uint8_t* seeds, hipStream_t st, const uint32_t* share_aff,
-                               uint32_t n_nodes, const int32_t* pre_status) {
+                               uint32_t n_nodes, const int32_t* pre_status, const uint8_t* share_ok) {
     HBG_LAT_DISPATCH((uint64_t)n * (t + 1 <= 24 ? 16u : 32u),
                      launch_tdec_combine(n, t, share48, idx, V, V_off, out, status, scratch, seeds, st, share_aff,
-                                         n_nodes, pre_status));
+                                         n_nodes, pre_status, share_ok));
     HBG_COUNT_MARK("tdec_combine", st);
     if (n == 0) return hipSuccess;
     HBG_GRID_CHECK(n, 64);  // every grid of this call, before the first launch
     // scratch: >= 36 words per ciphertext (the MSM kernels' Jacobian sums)
     if (t + 1 <= 24)
         tdec_combine_msm<16, 24><<<dim3((n + 3) / 4), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
-                                                                         share_aff, n_nodes, pre_status);
+                                                                         share_aff, n_nodes, pre_status, share_ok);
     else if (t + 1 <= 32)
         tdec_combine_msm<32, 32><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
-                                                                         share_aff, n_nodes, pre_status);
+                                                                         share_aff, n_nodes, pre_status, share_ok);
     else if (t + 1 <= 64)  // two shares a lane: ~28 % fewer Fp products per ciphertext than <64, 64> at t = 42
         tdec_combine_msm<32, 64><<<dim3((n + 1) / 2), dim3(64), 0, st>>>(n, t, share48, idx, scratch, status,
-                                                                         share_aff, n_nodes, pre_status);
+                                                                         share_aff, n_nodes, pre_status, share_ok);
     else
         tdec_combine<<<dim3((n + 63) / 64), dim3(64), 0, st>>>(n, t, share48, idx, seeds, status, scratch);
     hipError_t e = hipGetLastError();
@@ -3209,11 +3208,12 @@ hipError_t launch_sig_doc_prepare(uint32_t n, const uint8_t* doc, const uint64_t
 hipError_t launch_sig_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uint32_t n_doc, const BatchDesc* desc,
                                    const uint32_t* perm, const uint8_t* share96, const uint32_t* share_pk,
                                    const uint8_t* seeds, const uint32_t* pk_aff, const int32_t* pk_status,
-                                   const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, hipStream_t st) {
+                                   const uint32_t* pk_tbl, uint32_t* sums, uint8_t* leaf_ok, const BatchKey& key,
+                                   hipStream_t st) {
     HBG_COUNT_MARK("sig_batch_leaves", st);
     if (nb_max == 0) return hipSuccess;
     sig_batch_leaves<<<dim3(nb_max), dim3(64), 0, st>>>(nb_max, nb_dev, n_doc, desc, perm, share96, share_pk, seeds, pk_aff,
-                                                        pk_status, pk_tbl, sums, leaf_ok);
+                                                        pk_status, pk_tbl, sums, leaf_ok, key);
     return hipGetLastError();
 }
 // lines: kResidentBlocks * 64 G2Prepared slots (one per lane of a launch chunk)

@@ -179,13 +179,35 @@ int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards
  * V_off[n_ct + 1] offsets (entry k = V[V_off[k] .. V_off[k+1])).
  */
 
+/* Share-verification schedule of hbg_tdec_verify_shares,
+ * hbg_tdec_threshold_decrypt and hbg_sig_verify_shares (per context):
+ *  - HBG_VERIFY_PER_SHARE: one independent pairing equation per share, the
+ *    crate's own check — every bit is deterministic and identical to the
+ *    crate's bool.
+ *  - HBG_VERIFY_BATCHED (the default): from 393,216 shares per call up, the
+ *    shares of one ciphertext (document) are checked in weighted batches of
+ *    <= 64 by a small-exponent test with binary splitting down to single
+ *    shares; smaller calls run per share.  Every 0 bit is the crate's per-share
+ *    verdict.  A 1 bit comes from a passing (sub)batch and equals the crate's
+ *    bool except with probability <= 2^-127 per (sub)batch check that holds an
+ *    invalid share: the weights are 127-bit (a + b x^2, a odd, a and b 64-bit)
+ *    and derived from a secret 32-byte key drawn from getrandom(2) at hbg_init
+ *    and never exposed, so a sender can neither predict nor grind them.
+ * Returns HBG_E_ARG for any other mode. */
+#define HBG_VERIFY_BATCHED 0
+#define HBG_VERIFY_PER_SHARE 1
+int hbg_set_share_verify(hbg_ctx *ctx, int mode);
+
 /* PublicKeyShare::verify_decryption_share for n_shares shares:
  * share k (share48[k]) claims to decrypt ciphertext share_ct[k] under public
  * key share pk48[share_pk[k]] (PublicKeySet::public_key_share(i) values).
  * ok[k] = 1 iff every point decodes (in its subgroup), the ciphertext decodes,
- * and e(share, hash_g1_g2(U, V)) == e(pk, W).  Bit-identical to the crate's
- * bool for points the crate would deserialise.  share_ct[k] >= n_ct or
- * share_pk[k] >= n_pk: HBG_E_ARG (device mode: ok[k] = 0, device-side). */
+ * and e(share, hash_g1_g2(U, V)) == e(pk, W), for points the crate would
+ * deserialise: identical to the crate's bool under HBG_VERIFY_PER_SHARE, and
+ * under the default HBG_VERIFY_BATCHED up to the 2^-127 bound stated at
+ * hbg_set_share_verify (a 0 is always the crate's verdict).  share_ct[k] >=
+ * n_ct or share_pk[k] >= n_pk: HBG_E_ARG (device mode: ok[k] = 0,
+ * device-side). */
 int hbg_tdec_verify_shares(hbg_ctx *ctx, uint32_t n_ct, const uint8_t *U48, const uint8_t *V,
                            const uint64_t *V_off, const uint8_t *W96, uint32_t n_pk,
                            const uint8_t *pk48, uint64_t n_shares, const uint8_t *share48,
@@ -242,8 +264,10 @@ int hbg_tdec_combine(hbg_ctx *ctx, uint32_t t, uint32_t n_ct, const uint8_t *sha
  * never arrive are not read for the output); pk48 [n_nodes][48] the public
  * key shares; outcome [n_ct][n_nodes] (one HBG_SHARE_* code, optionally |
  * HBG_SHARE_REPEAT).  Every share is verified on the device (batched, as
- * hbg_tdec_verify_shares); plaintext bytes of a ciphertext with status != 0
- * are unspecified. */
+ * hbg_tdec_verify_shares, under the context's hbg_set_share_verify schedule);
+ * a validator's own share is never verified: it is decompressed for the
+ * combination, and one that does not decode gives HBG_E_INVALID_POINT.
+ * Plaintext bytes of a ciphertext with status != 0 are unspecified. */
 #define HBG_SHARE_NONE 0u     /* no message from this sender (or not processed)        */
 #define HBG_SHARE_ACCEPTED 1u /* valid, held before termination                         */
 #define HBG_SHARE_FAULTY 2u   /* invalid before termination: UnverifiedDecryptionShareSender */
@@ -319,12 +343,13 @@ int hbg_sig_combine(hbg_ctx *ctx, uint32_t t, uint64_t n, const uint8_t *share96
 /* PublicKeyShare::verify(share, doc) for n signature shares grouped by
  * document (the coin nonce every node signs): share k (share96[k]) claims to
  * sign doc share_doc[k] (doc[doc_off[d] .. doc_off[d+1]]) under public key
- * share pk48[share_pk[k]].  ok[k] is bit-identical to hbg_bls_verify on the
- * same (pk, doc, share): 1 iff the key and the share decode (subgroup checks)
- * and e(pk, hash_g2(doc)) == e(G1, share).  hash_g2 runs once per document
- * and shares of one document are checked in weighted batches (a failing
- * batch falls back to the per-share equation); hbg_test_set_tdec_batched(ctx, 0)
- * selects the per-share schedule.  Out-of-range indices as in
+ * share pk48[share_pk[k]].  ok[k] = 1 iff the key and the share decode
+ * (subgroup checks) and e(pk, hash_g2(doc)) == e(G1, share): identical to
+ * hbg_bls_verify on the same (pk, doc, share) under HBG_VERIFY_PER_SHARE, and
+ * under the default HBG_VERIFY_BATCHED up to the 2^-127 bound stated at
+ * hbg_set_share_verify.  hash_g2 runs once per document; from 393,216 shares
+ * up the shares of one document are checked in weighted batches (a failing
+ * batch is split down to the per-share equation).  Out-of-range indices as in
  * hbg_tdec_verify_shares.  Replaces
  * hbbft ThresholdSign::handle_message's PublicKeyShare::verify (reached from
  * src/hydrabadger/state.rs:487). */

@@ -59,6 +59,8 @@ pub const HBG_WIRE_KIND_MESSAGE: u32 = 7;
 pub const HBG_WIRE_KIND_KEYGEN: u32 = 9;
 pub const HBG_WIRE_KIND_MAX: u32 = 10;
 pub const HBG_WIRE_MAX_FRAME: u32 = 8 * 1024 * 1024;
+pub const HBG_VERIFY_BATCHED: c_int = 0;
+pub const HBG_VERIFY_PER_SHARE: c_int = 1;
 
 extern "C" {
     pub fn hbg_init(out: *mut *mut hbg_ctx, device: c_int) -> c_int;
@@ -91,6 +93,7 @@ extern "C" {
     pub fn hbg_rbc_decode(ctx: *mut hbg_ctx, n_nodes: u32, shard_len: u64, shards: *mut u8, shard_stride: u64,
                           present: *const u8, roots: *const u8, payload_out: *mut u8, payload_stride: u64,
                           payload_len: *mut u64, status: *mut u8, n: u64, flags: u32) -> c_int;
+    pub fn hbg_set_share_verify(ctx: *mut hbg_ctx, mode: c_int) -> c_int;
     pub fn hbg_tdec_verify_shares(ctx: *mut hbg_ctx, n_ct: u32, u48: *const u8, v: *const u8, v_off: *const u64,
                                   w96: *const u8, n_pk: u32, pk48: *const u8, n_shares: u64, share48: *const u8,
                                   share_ct: *const u32, share_pk: *const u32, ok: *mut u8, flags: u32) -> c_int;

@@ -89,3 +89,25 @@ def test_bench_backend_switch_parses():
             bench.parse()
     finally:
         sys.argv = old
+
+
+def test_checks_final_is_last_and_sets_exit_status():
+    """The compact verdicts ride as the line's last key (the driver keeps the
+    tail of a long line) and a false check or a failed leg makes bench.py exit
+    non-zero; legs that did not run (None) do not count."""
+    ok = bench.checks(None, None, None, None, {"all_decrypted_ok": True}, None, {"all_ok": True}, None)
+    line = {"value": 1.0, "checks": ok, "leg_errors": None}
+    line["checks_final"] = bench.checks_final(line)
+    assert list(line)[-1] == "checks_final"
+    assert line["checks_final"] == {"epoch_all_decrypted_ok": True, "coin_all_ok": True, "leg_errors": [],
+                                    "all_ok": True}
+    assert bench.exit_status(line) == 0
+    bad = dict(line, checks=bench.checks({"oracle_match": False}, None, None, None, None, None, None, None))
+    bad["checks_final"] = bench.checks_final(bad)
+    assert bad["checks_final"]["decode_oracle_match"] is False and bench.exit_status(bad) == 1
+    crashed = dict(line, leg_errors={"tdec": "RuntimeError: x"})
+    crashed["checks_final"] = bench.checks_final(crashed)
+    assert crashed["checks_final"]["leg_errors"] == ["tdec"] and bench.exit_status(crashed) == 1
+    none_ran = {"checks": bench.checks(*[None] * 8), "leg_errors": None}
+    none_ran["checks_final"] = bench.checks_final(none_ran)
+    assert bench.exit_status(none_ran) == 0

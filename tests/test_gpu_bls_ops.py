@@ -243,6 +243,43 @@ def test_coin_share_verify_batched(seed, bad_rate):
         assert np.array_equal(o, expect)
 
 
+def test_coin_share_cancelling_pair_rejected():
+    """§8(f3) coin shares: sig_a + D and sig_b - D (G2) for two signers of one
+    document — an unweighted batch sum would pass — both 0 on every schedule
+    and under HBG_VERIFY_PER_SHARE; the other shares 1."""
+    th = _th()
+    from hydrabadger_amd import _lib
+    s = scenario()
+    ks, n = s["ks"], len(s["pk_shares"])
+    sks = [ks.secret_key_share(i) for i in range(n)]
+    pks = [B.g1_compress(p) for p in s["pk_shares"]]
+    docs = [b"coin nonce 0", b"coin nonce 1"]
+    signed = th.sign_batch(sks, [(i, d) for d in docs for i in range(n)])
+    D = B.g2_mul(B.G2, 987654321)
+    items, expect = [], []
+    for d in range(len(docs)):
+        for rep in range(10):          # 70 shares a document: batches of 64 + 6
+            for i in range(n):
+                sg = signed[d * n + i]
+                if d == 0 and rep == 2 and i in (1, 4):
+                    p = B.g2_decompress(sg)
+                    sg = B.g2_compress(B.g2_add(p, D if i == 1 else B.g2_neg(D)))
+                    expect.append(0)
+                else:
+                    expect.append(1)
+                items.append((d, i, sg))
+    expect = np.array(expect, np.uint8)
+    ctx = _lib.Context(0)
+    try:
+        for mode in (1, 2, 3, 0):
+            _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
+            assert np.array_equal(th.verify_sig_shares_batch(pks, docs, items, ctx), expect), mode
+        ctx.set_share_verify(_lib.HBG_VERIFY_PER_SHARE)
+        assert np.array_equal(th.verify_sig_shares_batch(pks, docs, items, ctx), expect)
+    finally:
+        ctx.close()
+
+
 def test_long_contributions_encrypt_verify_decrypt():
     """HoneyBadger threshold-encrypts the whole serialised contribution, so V
     is as long as a proposal (BASELINE.json configs[4]: 1 MiB).  encrypt_with_rng

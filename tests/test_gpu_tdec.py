@@ -300,6 +300,56 @@ def test_batched_verify_equals_per_share(bad_rate, seed):
         assert np.array_equal(o, expect)
 
 
+def test_cancelling_pair_rejected_on_every_schedule():
+    """Two invalid shares whose errors cancel in an unweighted sum —
+    S_a + D and S_b - D for sender a, b's true shares S_a, S_b of one
+    ciphertext — planted in one batch of 64 (and again across two
+    ciphertexts' batches): the batch sum with equal weights would pass, the
+    secret 127-bit weights make it fail, and the binary splitting reaches both
+    singles, so both bits are 0 on every schedule (test hook 1, 2, 3, 0) and
+    under the production HBG_VERIFY_PER_SHARE flag; every other share is 1.
+    An unknown schedule mode is refused."""
+    import json
+    import os
+    from hydrabadger_amd import _lib
+    th = _th()
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "tdec_n64.json")))["scenario"]
+    K, n = len(g["cts"]), len(g["pk_shares"])
+    cts = [th.Ciphertext(bytes.fromhex(c["U"]), bytes.fromhex(c["V"]), bytes.fromhex(c["W"])) for c in g["cts"]]
+    pk = [bytes.fromhex(p) for p in g["pk_shares"]]
+    D = B.g1_mul(B.G1, 0x1234567890ABCDEF)
+    shares = [[bytes.fromhex(x) for x in c["shares"]] for c in g["cts"]]
+
+    def shifted(j, i, sign):
+        p = B.g1_decompress(shares[j][i])
+        return B.g1_compress(B.g1_add(p, D if sign > 0 else B.g1_neg(D)))
+
+    items, expect = [], []
+    for j in range(K):
+        for i in range(n):
+            if (j, i) in ((0, 3), (1, 17), (2, 60)):
+                items.append((shifted(j, i, +1), j, i)); expect.append(0)
+            elif (j, i) in ((0, 41), (1, 18), (3, 5)):
+                items.append((shifted(j, i, -1), j, i)); expect.append(0)
+            else:
+                items.append((shares[j][i], j, i)); expect.append(1)
+    expect = np.array(expect, np.uint8)
+    ctx = _lib.Context(0)
+    try:
+        for mode in (1, 2, 3, 0):
+            _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
+            assert np.array_equal(th.verify_shares_batch(cts, pk, items, ctx), expect), mode
+        _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, 3))
+        ctx.set_share_verify(_lib.HBG_VERIFY_PER_SHARE)     # overrides the test hook
+        assert np.array_equal(th.verify_shares_batch(cts, pk, items, ctx), expect)
+        ctx.set_share_verify(_lib.HBG_VERIFY_BATCHED)
+        assert np.array_equal(th.verify_shares_batch(cts, pk, items, ctx), expect)
+        with pytest.raises(_lib.HbgError):
+            ctx.set_share_verify(2)
+    finally:
+        ctx.close()
+
+
 def test_batched_lines_beside_leaves():
     """8,200 ciphertexts (the fixture's 4 replicated) x 64 shares, 1 % bad:
     with 8,193..32,768 ciphertexts the batched schedule builds H (sponge

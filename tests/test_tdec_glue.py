@@ -163,6 +163,56 @@ def test_gpu_glue_matches_oracle_hand_cases():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 3])
+def test_gpu_glue_own_share_unverified(mode):
+    """A validator's own share is inserted unverified (hbbft start_decryption),
+    so the combine cannot take its point from the verification's decoded-point
+    table: an own share that does not decode gives HBG_E_INVALID_POINT (with
+    the own sender ACCEPTED, as the oracle's outcome), and an own public key
+    share that does not decode (its network shares all fail) still combines
+    the trusted own share into the right plaintext.  A first call on other
+    ciphertexts fills the context's scratch, so a stale table entry would show
+    as a wrong plaintext.  On the per-share (0) and batched (3) schedules."""
+    from hydrabadger_amd import _lib
+    th = _th()
+    sc, other = _case(), _case(seed=9)
+    t, n = sc["t"], len(sc["pk_shares"])
+    pks = [B.g1_compress(p) for p in sc["pk_shares"]]
+    O = T.ARRIVAL_OWN
+    enc = lambda c: th.Ciphertext(B.g1_compress(c.U), c.V, B.g2_compress(c.W))  # noqa: E731
+    ctx = _lib.Context(0)
+    try:
+        _lib.check(_lib.lib().hbg_test_set_tdec_batched(ctx.h, mode))
+        pts, st, _ = th.threshold_decrypt_batch(
+            t, [enc(c) for c in other["cts"]], [B.g1_compress(p) for p in other["pk_shares"]],
+            [[B.g1_compress(x) for x in row] for row in other["shares"]], None, ctx)
+        assert list(st) == [0] * len(other["cts"]) and pts == other["msgs"]
+        # (1) own share 2 of ct 0 undecodable; ct 1 the same list with a valid own share
+        sh = [[B.g1_compress(x) for x in row] for row in sc["shares"]]
+        junk = bytearray(sh[0][2]); junk[0] &= 0x7F
+        sh[0][2] = bytes(junk)
+        arr = [[O | 2, 0, 1, 3], [O | 2, 0, 1, 3], [O | 2, 0, 1, 3]]
+        pts, st, oc = th.threshold_decrypt_batch(t, [enc(c) for c in sc["cts"]], pks, sh, arr, ctx)
+        assert st[0] == _lib.HBG_E_INVALID_POINT and oc[0][2] == ACC
+        for k in (1, 2):
+            rst, rpt, roc = T.threshold_decrypt(t, sc["cts"][k], sc["pk_shares"], sc["shares"][k], arr[k])
+            assert st[k] == rst == 0 and pts[k] == rpt == sc["msgs"][k] and list(oc[k]) == roc
+        # (2) own pk share 4 undecodable: node 4's network shares fail, its own share is trusted
+        bad_pks = list(pks)
+        jp = bytearray(bad_pks[4]); jp[0] &= 0x7F
+        bad_pks[4] = bytes(jp)
+        sh = [[B.g1_compress(x) for x in row] for row in sc["shares"]]
+        arr = [[0, O | 4, 1, 2], [O | 4, 5, 6, 3], [4, O | 4, 1, 2]]
+        pts, st, oc = th.threshold_decrypt_batch(t, [enc(c) for c in sc["cts"]], bad_pks, sh, arr, ctx)
+        for k in range(3):
+            assert st[k] == 0 and pts[k] == sc["msgs"][k], k
+            assert oc[k][4] == ACC, k
+        assert list(oc[0]) == [ACC, ACC, IGN, NONE, ACC, NONE, NONE]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", [1, 2])
 def test_gpu_glue_random_epochs_match_oracle(seed):
     """16 nodes (t = 5), 12 ciphertexts: seeded arrival orders (some lists cut
