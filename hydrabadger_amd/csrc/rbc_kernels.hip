@@ -1542,12 +1542,12 @@ hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32
     const uint32_t nodes = merkle_nodes(N);
     const uint64_t maxlen = (uint64_t)D * L;
     const uint32_t bpi = (uint32_t)(((maxlen + 15) / 16 + 255) / 256);
-    HBG_GRID_CHECK(n * bpi, 256);
+    HBG_GRID_CHECK(n * bpi, 256);  // every grid of this call, before the first launch
+    HBG_GRID_CHECK(n, 256);
     rbc_glue_status<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(shards, S, L, N, D, n, levels, nodes,
                                                                             roots, rstatus, plen, status);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    HBG_GRID_CHECK(n, 256);
     rbc_glue_clear<<<dim3((uint32_t)n), dim3(256), 0, st>>>(n, maxlen, status, out, ostride);
     e = hipGetLastError();
     if (e != hipSuccess || !copy) return e;

@@ -916,7 +916,14 @@ BD void lds_sqr(uint64_t* f) {
 template <bool JAC>
 BD Fp12 miller_loop2(const uint32_t* c1, const Fp& a1, const Fp& b1, const Fp& z1, bool use1, const uint32_t* c2,
                      const Fp& a2, const Fp& b2, const Fp& z2, bool use2) {
-    __shared__ uint64_t f_lds[72 * 64];  // one wave per workgroup (TDEC kernels: __launch_bounds__(64))
+    // one accumulator per lane, lane-strided: correct for workgroups of at most
+    // 64 lanes.  Every caller is a TDEC_KERNEL / TDEC_WAVE1_KERNEL, whose
+    // __launch_bounds__(64) makes a larger launch fail at launch time; the
+    // diagnostic build also traps here.
+    __shared__ uint64_t f_lds[72 * 64];
+#ifdef HBG_DEBUG_CHECKS
+    if (blockDim.x * blockDim.y * blockDim.z > 64) __builtin_trap();
+#endif
     uint64_t* f = f_lds + threadIdx.x;
     lds_st_fp6(f, 0, fp6_one());
     lds_st_fp6(f, 1, fp6_zero());
@@ -942,6 +949,8 @@ BD Fp12 miller_loop2(const uint32_t* c1, const Fp& a1, const Fp& b1, const Fp& z
 }
 
 // one pairing check: prod e(P_i, Q_i) == 1 over the two prepared pairs
+// (miller_loop2's LDS accumulator: callable only from kernels of <= 64 lanes
+// a workgroup — the TDEC kernel macros' __launch_bounds__(64))
 BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool use1, const uint32_t* c2,
                        const Fp& p2x, const Fp& p2y, bool use2) {
     Fp12 f = miller_loop2<false>(c1, p1x, p1y, p1y, use1, c2, p2x, p2y, p2y, use2);
@@ -949,7 +958,8 @@ BD bool pairing_check2(const uint32_t* c1, const Fp& p1x, const Fp& p1y, bool us
     return fp12_is_one(f);
 }
 
-// e(P1, Q1) e(P2, Q2) in GT for Jacobian P1, P2 (an identity point: its pair is skipped)
+// e(P1, Q1) e(P2, Q2) in GT for Jacobian P1, P2 (an identity point: its pair is
+// skipped; <= 64-lane workgroups, as pairing_check2)
 BD Fp12 pairing_value2_jac(const uint32_t* c1, const G1& p1, const uint32_t* c2, const G1& p2, bool use2) {
     const bool u1 = !fp_is_zero(p1.z), u2 = use2 && !fp_is_zero(p2.z);
     const Fp z1 = fp_sqr(p1.z), z2 = fp_sqr(p2.z);

@@ -47,6 +47,15 @@ impl Engine {
         Ok(Engine { ctx: Mutex::new(ctx) })
     }
 
+    /// Share-verification schedule (`hbg_set_share_verify`): `per_share =
+    /// true` makes every decryption / coin share bit the crate's own
+    /// per-share pairing equation (deterministic); the default batched
+    /// schedule differs from it with probability <= 2^-127 per check.
+    pub fn set_share_verify_per_share(&self, per_share: bool) -> Result<(), Error> {
+        let mode = if per_share { HBG_VERIFY_PER_SHARE } else { HBG_VERIFY_BATCHED };
+        self.with(|c| check(unsafe { hbg_set_share_verify(c, mode) }))
+    }
+
     fn with<R>(&self, f: impl FnOnce(*mut hbg_ctx) -> R) -> R {
         let g = self.ctx.lock().unwrap();
         f(*g)

@@ -352,10 +352,14 @@ def test_cancelling_pair_rejected_on_every_schedule():
 
 def test_batched_lines_beside_leaves():
     """8,200 ciphertexts (the fixture's 4 replicated) x 64 shares, 1 % bad:
-    with 8,193..32,768 ciphertexts the batched schedule builds H (sponge
-    inline) and W's line tables in one grid beside the share leaves
-    (api.hip launch_lines, tdec_ct_prepare_hw); its bits equal the fixture's
-    per-share truth."""
+    with 8,193..131,072 ciphertexts (api.hip kLinesBesideLeavesMin/Max) the
+    batched schedule builds H (sponge inline) and W's line tables in one grid
+    beside the share leaves (launch_lines, tdec_ct_prepare_hw); its bits equal
+    the fixture's per-share truth.  The other two branches of launch_lines:
+    below 8,193 ciphertexts (W on the aux stream, H on the main one) with
+    round-capacity overflow into the per-share round —
+    test_batched_verify_equals_per_share's 150 ciphertexts at 30 % / 100 %
+    bad; above 131,072 — test_batched_lines_above_beside_max."""
     import json
     import os
     from hydrabadger_amd import _lib
@@ -378,6 +382,32 @@ def test_batched_lines_beside_leaves():
     finally:
         ctx.close()
     assert np.array_equal(out, expect)
+
+
+def test_batched_lines_above_beside_max():
+    """131,200 device-generated ciphertexts x 16 shares (2 % bad, three
+    kinds): past kLinesBesideLeavesMax the deferred line tables fall back to
+    W on the aux stream and H (SHA3(V) by tdec_v_digest) on the main stream;
+    every bit equals construction."""
+    torch = pytest.importorskip("torch")
+    from hydrabadger_amd import _lib, tdec_workload as tw
+    dev = torch.device("cuda:0")
+    ctx = _lib.Context(0)
+    try:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        n_ct, N = 131_200, 16
+        ep = tw.make_epoch(ctx, dev, n_ct=n_ct, n_nodes=N, msg_len=32, bad_rate=0.02, seed=5)
+        n = n_ct * N
+        sct = torch.arange(n_ct, dtype=torch.int32, device=dev).repeat_interleave(N)
+        spk = torch.arange(N, dtype=torch.int32, device=dev).repeat(n_ct)
+        ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+        _lib.check(_lib.lib().hbg_tdec_verify_shares(ctx.h, n_ct, ep.U.data_ptr(), ep.V.data_ptr(),
+                                                     ep.V_off.data_ptr(), ep.W.data_ptr(), N, ep.pk48.data_ptr(), n,
+                                                     ep.share48.data_ptr(), sct.data_ptr(), spk.data_ptr(),
+                                                     ok.data_ptr(), _lib.HBG_DEVICE), "verify_decryption_share")
+        assert np.array_equal(ok.cpu().numpy().reshape(n_ct, N).astype(bool), ~ep.bad)
+    finally:
+        ctx.close()
 
 
 def test_g1_mul_u64_and_add():
