@@ -106,6 +106,29 @@ def parse():
     return ap.parse_args()
 
 
+def head_digest() -> str:
+    """The kernels this tree builds (hydrabadger_amd.build.source_digest)."""
+    from hydrabadger_amd.build import source_digest
+    return source_digest()
+
+
+def measured_at_head(d: dict) -> bool | None:
+    """Whether a committed profile was measured on the kernels of this tree
+    (its csrc_sha16 stamp, tools/pack_profiles.py / tools/fpcount.py); None
+    for a profile older than the stamp."""
+    sha = d.get("csrc_sha16") or (d.get("_meta") or {}).get("csrc_sha16")
+    return None if sha is None else sha == head_digest()
+
+
+def newest(*rel: str) -> str:
+    """The first of the candidate profile paths that exists (newest first)."""
+    for r in rel:
+        p = os.path.join(ROOT, *r.split("/"))
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, *rel[-1].split("/"))
+
+
 def pmc_traffic(instances: int) -> dict:
     """HBM bytes per launch measured by rocprofv3 PMC passes (FETCH_SIZE x2 +
     WRITE_SIZE, separate runs: tools/pmc.sh) at this launch shape, from
@@ -121,6 +144,9 @@ def pmc_traffic(instances: int) -> dict:
             out[k] = d[k]["hbm_bytes_per_launch"]
             # a kernel measured in a later pass names its own summary
             out[k + "_source"] = d[k].get("summary", d.get("summary", ""))
+            out[k + "_measured_at_head"] = measured_at_head(d[k])
+            if d[k].get("valu_insts_per_wave"):
+                out[k + "_valu_insts_per_wave"] = d[k]["valu_insts_per_wave"]
     return out
 
 
@@ -133,7 +159,7 @@ DECODE_KERNELS = ("rs_plan", "rs_code_movrel", "rs_encode_missing", "merkle_buil
 
 
 def decode_pmc_traffic(instances: int) -> dict:
-    path = os.path.join(ROOT, "profiles", "r04", "pmc_decode_fused_8192.json")
+    path = newest("profiles/r06/pmc_decode_fused_8192.json", "profiles/r04/pmc_decode_fused_8192.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -147,7 +173,10 @@ def decode_pmc_traffic(instances: int) -> dict:
             by[short] = v["hbm_read_bytes_corrected"] + v.get("hbm_write_bytes", 0.0)
     if not by:
         return {}
-    return {"bytes_per_call": sum(by.values()), "by_kernel": by, "source": os.path.relpath(path, ROOT)}
+    vw = {name.split("<")[0]: v.get("valu_insts_per_wave") for name, v in d.items()
+          if isinstance(v, dict) and name.split("<")[0] == "rbc_decode_merkle"}
+    return {"bytes_per_call": sum(by.values()), "by_kernel": by, "source": os.path.relpath(path, ROOT),
+            "valu_insts_per_wave": vw.get("rbc_decode_merkle"), "measured_at_head": measured_at_head(d)}
 
 
 def timed(fn, reps: int):
@@ -211,6 +240,7 @@ def fp_count_profile(n_nodes: int, t: int, bad_rate: float) -> dict:
     if (sh.get("n_nodes"), sh.get("t"), sh.get("bad_rate")) != (n_nodes, t, bad_rate):
         return {}
     d["path"] = os.path.relpath(path, ROOT)
+    d["measured_at_head"] = measured_at_head(d)
     return d
 
 
@@ -244,7 +274,7 @@ def tdec_pmc_traffic(n_shares: int) -> dict:
     WRITE_SIZE per dispatch, profiles/r05/pmc_tdec_100k.json over
     tools/tdec_kbench.py --cts 100000: the LDS Miller accumulator and the
     binary check rounds); per-dispatch averages times the dispatches per call."""
-    path = os.path.join(ROOT, "profiles", "r05", "pmc_tdec_100k.json")
+    path = newest("profiles/r06/pmc_tdec_100k.json", "profiles/r05/pmc_tdec_100k.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -263,7 +293,8 @@ def tdec_pmc_traffic(n_shares: int) -> dict:
     return {"bytes_per_call": total, "bytes_per_share": total / n_shares,
             "per_kernel_bytes_per_share": {k: v / n_shares for k, v in sorted(per_kernel.items(), key=lambda x: -x[1])},
             "source": os.path.relpath(path, ROOT) + " (tools/pmc_tdec.sh, KB_ARGS='--cts 100000 --reps 1', "
-                      "EXTRA_GROUPS='FETCH_SIZE WRITE_SIZE')"}
+                      "EXTRA_GROUPS='FETCH_SIZE WRITE_SIZE')",
+            "kernels_measured": sorted(per_kernel), "measured_at_head": measured_at_head(d)}
 
 
 def fp_count_floor() -> dict:
@@ -410,6 +441,7 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             "verify_only": {"achieved": achieved_v / 1e12, "frac": achieved_v / MAD_PEAK,
                             "fp_mul_per_share": per_share_v},
             "traffic": None, "count_source": prof["path"] + " (" + prof.get("source", "") + ")",
+            "count_measured_at_head": prof.get("measured_at_head"),
             "count_note": "counted at this round's kernels by the branch-free instrumented build (one atomic add per "
                           "active lane per Fp product; DESIGN.md §4 'The HBG_FP_COUNT fault'), outputs checked "
                           "against the product's",
@@ -433,6 +465,8 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             out["roofline"]["traffic_per_share"] = tr["bytes_per_share"]
             out["roofline"]["traffic_per_share_by_kernel"] = tr["per_kernel_bytes_per_share"]
             out["roofline"]["traffic_source"] = tr["source"]
+            out["roofline"]["traffic_kernels_measured"] = tr["kernels_measured"]
+            out["roofline"]["traffic_measured_at_head"] = tr["measured_at_head"]
     return out, ep
 
 
@@ -996,6 +1030,8 @@ def main():
         "achieved": achieved_ops / 1e12, "peak": VALU_PEAK / 1e12, "frac": achieved_ops / VALU_PEAK,
         "traffic": traffic.get("rbc_encode_merkle_22_42"), "traffic_unit": "HBM bytes per launch (PMC)",
         "traffic_source": traffic.get("rbc_encode_merkle_22_42_source") or traffic.get("source"),
+        "traffic_measured_at_head": traffic.get("rbc_encode_merkle_22_42_measured_at_head"),
+        "valu_insts_per_wave_pmc": traffic.get("rbc_encode_merkle_22_42_valu_insts_per_wave"),
         "traffic_vs_alg_bytes": (traffic["rbc_encode_merkle_22_42"] / (fused_bytes * B)
                                  if traffic.get("rbc_encode_merkle_22_42") else None),
         "alg_ops_per_instance": ops + enc_ops, "keccak_ops_per_instance": ops, "encoder_ops_per_instance": enc_ops,
@@ -1063,7 +1099,9 @@ def main():
                              "traffic": tr.get("bytes_per_call"), "traffic_unit": "HBM bytes per decode call (PMC)",
                              "traffic_vs_alg_bytes": (tr["bytes_per_call"] / (d_bytes * nd)
                                                       if tr.get("bytes_per_call") else None),
-                             "traffic_by_kernel": tr.get("by_kernel"), "traffic_source": tr.get("source")}}
+                             "traffic_by_kernel": tr.get("by_kernel"), "traffic_source": tr.get("source"),
+                             "traffic_measured_at_head": tr.get("measured_at_head"),
+                             "valu_insts_per_wave_pmc": tr.get("valu_insts_per_wave")}}
 
     decode = run_leg("decode", decode_leg) if not a.no_decode and "decode" in legs else None
     bwire = (run_leg("bwire", lambda: broadcast_wire_leg(ctx, dev, shards, levels, L, min(a.wire_instances, B), reps))

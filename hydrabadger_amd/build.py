@@ -57,6 +57,20 @@ def _compile(src: str, force: bool) -> tuple:
     return obj, not fresh
 
 
+def source_digest() -> str:
+    """16 hex digits of SHA-256 over every csrc/ file (name + bytes, sorted):
+    the identity of the kernels a profile was measured on.  Profiles under
+    profiles/ carry it as `csrc_sha16`; bench.py compares it with the tree it
+    runs from and reports `measured_at_head`."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        path = os.path.join(CSRC, f)
+        if os.path.isfile(path):
+            h.update(f.encode() + b"\0" + open(path, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, jobs: int | None = None) -> str:
     os.makedirs(OBJ, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))

@@ -829,8 +829,14 @@ BD G2 g2_dbl_v(const G2& p) {
 // G2 point steps stay out of line (one call per step of a scalar
 // multiplication / G2Prepared: keeps the G2 kernels' code and compile time
 // bounded).  Only one-wave-per-SIMD kernels call them (TDEC_WAVE1_KERNEL), so
-// every caller shares their 512-register budget.
-__device__ __noinline__ void g2_dbl_p(G2* r, const G2* p) { *r = g2_dbl_v(*p); }
+// every caller shares their 512-register budget.  (-DHBG_G2_STEP_INLINE: tool
+// builds of tools/ctw_probe.py only, the steps inlined into the kernel.)
+#ifdef HBG_G2_STEP_INLINE
+#define HBG_G2_STEP BD
+#else
+#define HBG_G2_STEP __device__ __noinline__
+#endif
+HBG_G2_STEP void g2_dbl_p(G2* r, const G2* p) { *r = g2_dbl_v(*p); }
 BD G2 g2_dbl(const G2& p) {
     G2 r;
     g2_dbl_p(&r, &p);
@@ -859,7 +865,7 @@ BD G2 g2_add_mixed_v(const G2& p, const Fp2& qx, const Fp2& qy) {
     return r;
 }
 
-__device__ __noinline__ void g2_add_mixed_p(G2* r, const G2* p, const Fp2* qx, const Fp2* qy) {
+HBG_G2_STEP void g2_add_mixed_p(G2* r, const G2* p, const Fp2* qx, const Fp2* qy) {
     *r = g2_add_mixed_v(*p, *qx, *qy);
 }
 BD G2 g2_add_mixed(const G2& p, const Fp2& qx, const Fp2& qy) {
@@ -958,7 +964,7 @@ BD LineCoeff g2_doubling_step_v(G2& r) {
 }
 
 // G2Prepared addition step (Algorithm 27)
-__device__ __noinline__ void g2_doubling_step_p(G2* r, LineCoeff* c) { *c = g2_doubling_step_v(*r); }
+HBG_G2_STEP void g2_doubling_step_p(G2* r, LineCoeff* c) { *c = g2_doubling_step_v(*r); }
 BD LineCoeff g2_doubling_step(G2& r) {
     LineCoeff c;
     g2_doubling_step_p(&r, &c);
@@ -993,7 +999,7 @@ BD LineCoeff g2_addition_step_v(G2& r, const Fp2& qx, const Fp2& qy) {
     return {t10, tt1, t9};
 }
 
-__device__ __noinline__ void g2_addition_step_p(G2* r, LineCoeff* c, const Fp2* qx, const Fp2* qy) {
+HBG_G2_STEP void g2_addition_step_p(G2* r, LineCoeff* c, const Fp2* qx, const Fp2* qy) {
     *c = g2_addition_step_v(*r, *qx, *qy);
 }
 BD LineCoeff g2_addition_step(G2& r, const Fp2& qx, const Fp2& qy) {

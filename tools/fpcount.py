@@ -82,7 +82,9 @@ def run(n_ct: int, out: str, bad_rate: float = 0.01):
         return k, sum(v["per_share"] for v in k.values())
     dk, dtot = table(drv)
     vk, vtot = table(ver)
+    from hydrabadger_amd.build import source_digest
     res = {"source": f"tools/fpcount.py run --n-ct {n_ct} (instrumented build, HBG_FP_COUNT)",
+           "csrc_sha16": source_digest(),
            "shape": {"n_nodes": N, "t": t, "bad_rate": bad_rate, "n_ct": n_ct, "msg_len": ep.msg_len},
            "unit": "Fp multiplications + squarings (each 288 v_mad_u64_u32)",
            "per_share_total": dtot, "per_share_verify_total": vtot, "kernels": dk, "verify_kernels": vk,
