@@ -299,14 +299,14 @@ def tdec_pmc_traffic(n_shares: int) -> dict:
 
 def fp_count_floor() -> dict:
     """The batched verifier's executed Fp count with no bad share (no group
-    testing, no per-share fallback): profiles/r05/fpcount_batched_0pct.json."""
-    path = os.path.join(ROOT, "profiles", "r05", "fpcount_batched_0pct.json")
+    testing, no per-share fallback): profiles/r06/ (or r05/) fpcount_batched_0pct.json."""
+    path = newest("profiles/r06/fpcount_batched_0pct.json", "profiles/r05/fpcount_batched_0pct.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return {}
     return {"per_share_total": d["per_share_total"], "per_share_verify_total": d["per_share_verify_total"],
-            "source": os.path.relpath(path, ROOT)}
+            "source": os.path.relpath(path, ROOT), "measured_at_head": measured_at_head(d)}
 
 
 def kernel_meta(names) -> dict:
@@ -458,6 +458,7 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
             out["roofline"]["executed_vs_no_bad_shares"] = per_share / floor["per_share_total"]
             out["roofline"]["verify_only"]["executed_vs_no_bad_shares"] = per_share_v / floor["per_share_verify_total"]
             out["roofline"]["floor_source"] = floor["source"]
+            out["roofline"]["floor_measured_at_head"] = floor["measured_at_head"]
         tr = tdec_pmc_traffic(n)
         if tr:
             out["roofline"]["traffic"] = tr["bytes_per_call"]

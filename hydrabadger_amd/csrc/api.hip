@@ -24,6 +24,7 @@
 #include "rbc_kernels.h"
 #include "tdec_kernels.h"
 #include "../../include/hbgpu_testing.h"
+#include "selftest_vectors.h"
 
 using namespace hbg;
 
@@ -360,6 +361,51 @@ int hbg_coding_matrix(uint32_t data, uint32_t parity, uint8_t* out) {
     return HBG_OK;
 }
 
+// Power-on known-answer self-test of the BLS12-381 kernels (round 6; DESIGN.md
+// §4 "The HBG_FP_COUNT fault"): the first hbg_init of a process runs
+// Ciphertext::verify and verify_decryption_share on the committed fixture
+// (selftest_vectors.h: 3 valid ciphertexts + one whose W belongs to another,
+// 21 valid shares + 3 invalid ones) through the product kernels — both BLS
+// builds (throughput, latency), per-share and batched schedules — and every
+// later hbg_init fails with HBG_E_DEVICE if one bit differs.  This turns a
+// code-generation defect of the kind the round-5/6 probes found (a silently
+// wrong subgroup check in a differently shaped build) into a loud refusal.
+namespace {
+std::once_flag g_self_test_once;
+int g_self_test_rc = HBG_OK;
+
+int run_self_test(hbg_ctx* c) {
+    using namespace hbg::selftest;
+    uint8_t ok[kShares > kCts ? kShares : kCts];
+    const uint64_t prev = hbg_test_set_latency_lanes(0);
+    int rc = HBG_OK;
+    for (int build = 0; build < 2 && rc == HBG_OK; ++build) {
+        hbg_test_set_latency_lanes(build ? ~0ull : 0ull);  // 0: throughput build, all: latency build
+        int r = hbg_ct_verify(c, kCts, kU48, kV, kVoff, kW96, ok, 0);
+        if (r != HBG_OK || memcmp(ok, kCtOk, kCts) != 0) {
+            rc = r != HBG_OK ? r : HBG_E_DEVICE;
+            fprintf(stderr, "hbgpu self-test: Ciphertext::verify (%s build) differs from the known answers\n",
+                    build ? "latency" : "throughput");
+            break;
+        }
+        for (int sched : {0, 3}) {  // one pairing per share; the batched small-exponent test
+            c->tdec_batched = sched;
+            r = hbg_tdec_verify_shares(c, kCts, kU48, kV, kVoff, kW96, kPks, kPk48, kShares, kShare48, kShareCt,
+                                       kSharePk, ok, 0);
+            if (r != HBG_OK || memcmp(ok, kShareOk, kShares) != 0) {
+                rc = r != HBG_OK ? r : HBG_E_DEVICE;
+                fprintf(stderr, "hbgpu self-test: verify_decryption_share (%s build, %s) differs from the known answers\n",
+                        build ? "latency" : "throughput", sched ? "batched" : "per share");
+                break;
+            }
+        }
+    }
+    c->tdec_batched = 1;
+    hbg_test_set_latency_lanes(prev);
+    return rc;
+}
+}  // namespace
+
 int hbg_init(hbg_ctx** out, int device) {
     if (!out) return HBG_E_ARG;
     *out = nullptr;
@@ -382,6 +428,11 @@ int hbg_init(hbg_ctx** out, int device) {
         (void)hipStreamDestroy(c->own);
         delete c;
         return HBG_E_DEVICE;
+    }
+    std::call_once(g_self_test_once, [c] { g_self_test_rc = run_self_test(c); });
+    if (g_self_test_rc != HBG_OK) {
+        hbg_free(c);
+        return g_self_test_rc;
     }
     *out = c;
     return HBG_OK;

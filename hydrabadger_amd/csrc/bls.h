@@ -86,9 +86,9 @@ __device__ __forceinline__ void fp_count(int which) {
 // Diagnostic tool builds only (tools/ctw_probe.py, -DHBG_FP_VERIFY): every
 // product is recomputed by a portable CIOS multiplication (compiler code, no
 // asm) and the first mismatch is recorded with its call site.
-#ifdef HBG_FP_VERIFY
-__device__ unsigned long long g_fp_verify[2];  // [0] mismatches, [1] checks
-__device__ uint32_t g_fp_verify_rec[64];       // site, lane, a[12], b[12], asm r[12], ref r[12]
+// (-DHBG_FP_PORTABLE, tool builds of tools/ctw_probe.py only: every product
+// is this portable compiler-generated CIOS — no inline asm anywhere.)
+#if defined(HBG_FP_VERIFY) || defined(HBG_FP_PORTABLE)
 __device__ __forceinline__ Fp fp_mul_ref(const Fp& a, const Fp& b) {
     uint32_t t[14];
 #pragma unroll
@@ -129,6 +129,10 @@ __device__ __forceinline__ Fp fp_mul_ref(const Fp& a, const Fp& b) {
     for (int j = 0; j < 12; ++j) r[j] = sub ? u[j] : r[j];
     return r;
 }
+#endif
+#ifdef HBG_FP_VERIFY
+__device__ unsigned long long g_fp_verify[2];  // [0] mismatches, [1] checks
+__device__ uint32_t g_fp_verify_rec[64];       // site, lane, a[12], b[12], asm r[12], ref r[12]
 __device__ __noinline__ void fp_verify(Fp a, Fp b, Fp r, int site) {
     const Fp ref = fp_mul_ref(a, b);
     uint32_t d = 0;
@@ -161,6 +165,9 @@ __device__ __noinline__ void fp_verify(Fp a, Fp b, Fp r, int site) {
 // identical products may be merged by the compiler).
 BD Fp fp_mul(Fp a, Fp b) {
     HBG_FP_COUNT_CALL(0);
+#ifdef HBG_FP_PORTABLE
+    return fp_mul_ref(a, b);
+#endif
     HBG_FP_VERIFY_INPUT(a_in, a);
     asm(HBG_FP_SUB_CALL("hbg_fpmul1") : "+{v[0:11]}"(a) : "{v[12:23]}"(b) : HBG_FP_SUB1_CLOBBERS);
     HBG_FP_VERIFY_CALL(a_in, b, a);
@@ -169,6 +176,9 @@ BD Fp fp_mul(Fp a, Fp b) {
 
 BD Fp fp_sqr(Fp a) {
     HBG_FP_COUNT_CALL(1);
+#ifdef HBG_FP_PORTABLE
+    return fp_mul_ref(a, a);
+#endif
     HBG_FP_VERIFY_INPUT(a_in, a);
     asm(HBG_FP_SUB_CALL("hbg_fpmul1") : "+{v[0:11]}"(a) : "{v[12:23]}"(a) : HBG_FP_SUB1_CLOBBERS);
     HBG_FP_VERIFY_CALL(a_in, a_in, a);
@@ -179,6 +189,11 @@ BD Fp fp_sqr(Fp a) {
 BD void fp_mul2(Fp& r0, Fp& r1, Fp a0, Fp b0, Fp a1, Fp b1) {
     HBG_FP_COUNT_CALL(0);
     HBG_FP_COUNT_CALL(0);
+#ifdef HBG_FP_PORTABLE
+    r0 = fp_mul_ref(a0, b0);
+    r1 = fp_mul_ref(a1, b1);
+    return;
+#endif
     HBG_FP_VERIFY_INPUT(x0, a0);
     HBG_FP_VERIFY_INPUT(x1, a1);
     asm(HBG_FP_SUB_CALL("hbg_fpmul2")
@@ -196,6 +211,12 @@ BD void fp_mul3(Fp& r0, Fp& r1, Fp& r2, Fp a0, Fp b0, Fp a1, Fp b1, Fp a2, Fp b2
     HBG_FP_COUNT_CALL(0);
     HBG_FP_COUNT_CALL(0);
     HBG_FP_COUNT_CALL(0);
+#ifdef HBG_FP_PORTABLE
+    r0 = fp_mul_ref(a0, b0);
+    r1 = fp_mul_ref(a1, b1);
+    r2 = fp_mul_ref(a2, b2);
+    return;
+#endif
     HBG_FP_VERIFY_INPUT(x0, a0);
     HBG_FP_VERIFY_INPUT(x1, a1);
     HBG_FP_VERIFY_INPUT(x2, a2);
@@ -836,7 +857,23 @@ BD G2 g2_dbl_v(const G2& p) {
 #else
 #define HBG_G2_STEP __device__ __noinline__
 #endif
-HBG_G2_STEP void g2_dbl_p(G2* r, const G2* p) { *r = g2_dbl_v(*p); }
+// (per-function variants of the same tool switch: _DBL, _ADD, _PREP)
+#if defined(HBG_G2_STEP_INLINE) || defined(HBG_G2_STEP_INLINE_DBL)
+#define HBG_G2_STEP_DBL BD
+#else
+#define HBG_G2_STEP_DBL __device__ __noinline__
+#endif
+#if defined(HBG_G2_STEP_INLINE) || defined(HBG_G2_STEP_INLINE_ADD)
+#define HBG_G2_STEP_ADD BD
+#else
+#define HBG_G2_STEP_ADD __device__ __noinline__
+#endif
+#if defined(HBG_G2_STEP_INLINE) || defined(HBG_G2_STEP_INLINE_PREP)
+#define HBG_G2_STEP_PREP BD
+#else
+#define HBG_G2_STEP_PREP __device__ __noinline__
+#endif
+HBG_G2_STEP_DBL void g2_dbl_p(G2* r, const G2* p) { *r = g2_dbl_v(*p); }
 BD G2 g2_dbl(const G2& p) {
     G2 r;
     g2_dbl_p(&r, &p);
@@ -865,7 +902,7 @@ BD G2 g2_add_mixed_v(const G2& p, const Fp2& qx, const Fp2& qy) {
     return r;
 }
 
-HBG_G2_STEP void g2_add_mixed_p(G2* r, const G2* p, const Fp2* qx, const Fp2* qy) {
+HBG_G2_STEP_ADD void g2_add_mixed_p(G2* r, const G2* p, const Fp2* qx, const Fp2* qy) {
     *r = g2_add_mixed_v(*p, *qx, *qy);
 }
 BD G2 g2_add_mixed(const G2& p, const Fp2& qx, const Fp2& qy) {
@@ -964,7 +1001,7 @@ BD LineCoeff g2_doubling_step_v(G2& r) {
 }
 
 // G2Prepared addition step (Algorithm 27)
-HBG_G2_STEP void g2_doubling_step_p(G2* r, LineCoeff* c) { *c = g2_doubling_step_v(*r); }
+HBG_G2_STEP_PREP void g2_doubling_step_p(G2* r, LineCoeff* c) { *c = g2_doubling_step_v(*r); }
 BD LineCoeff g2_doubling_step(G2& r) {
     LineCoeff c;
     g2_doubling_step_p(&r, &c);
@@ -999,7 +1036,7 @@ BD LineCoeff g2_addition_step_v(G2& r, const Fp2& qx, const Fp2& qy) {
     return {t10, tt1, t9};
 }
 
-HBG_G2_STEP void g2_addition_step_p(G2* r, LineCoeff* c, const Fp2* qx, const Fp2* qy) {
+HBG_G2_STEP_PREP void g2_addition_step_p(G2* r, LineCoeff* c, const Fp2* qx, const Fp2* qy) {
     *c = g2_addition_step_v(*r, *qx, *qy);
 }
 BD LineCoeff g2_addition_step(G2& r, const Fp2& qx, const Fp2& qy) {

@@ -18,7 +18,8 @@ every VGPR, SGPR and SCC, and reports
     its epilogue restores — is live (the interprocedural clobber masks the
     compiler uses for internal functions).
 
-Register-level only: lanes are not modelled (a VALU write under a partial
+AGPRs (a0..a255, the compiler's VGPR spill space on gfx950) are tracked like
+VGPRs (round 6).  Register-level only: lanes are not modelled (a VALU write under a partial
 EXEC is taken as a whole-register definition, v_writelane as a partial one).
 Exit status 1 if anything is reported.
 """
@@ -43,7 +44,9 @@ _TWO_DST = re.compile(r"v_(mad_u64_u32|mad_i64_i32|add_co_u32_e64|sub_co_u32_e64
 
 def regs(tok: str) -> list:
     out = []
-    for m in re.finditer(r"\b([vs])(\d+)\b|\b([vs])\[(\d+):(\d+)\]", tok):
+    for m in re.finditer(r"\b(vcc|vcc_lo|vcc_hi|m0)\b", tok):  # named registers a call may clobber
+        out.append(("n", {"vcc_lo": "vcc", "vcc_hi": "vcc"}.get(m.group(1), m.group(1))))
+    for m in re.finditer(r"\b([vsa])(\d+)\b|\b([vsa])\[(\d+):(\d+)\]", tok):
         if m.group(1):
             out.append((m.group(1), int(m.group(2))))
         else:
@@ -64,11 +67,15 @@ def parse(line: str):
         d, u = regs(args[0]), regs(",".join(args[1:]))  # a returning atomic writes its first operand
     elif _NODEF.match(op):
         d, u = [], regs(rest)
-        if op.startswith("v_cmp_") and "_e64" in op:
+        if op.startswith("v_cmp_") and ("_e64" in op or (args and args[0] in ("vcc", "vcc_lo"))):
             d, u = regs(args[0]), regs(",".join(args[1:]))
     else:
         nd = 2 if _TWO_DST.match(op) else 1
         d, u = regs(",".join(args[:nd])), regs(",".join(args[nd:]))
+    if op.endswith("_e32") and len(args) >= 2 and args[1] == "vcc" and "_co_" in op:
+        # VOP2 carry ops: the second operand is the carry-out (a def); a carry-in is the last operand
+        d = list(d) + [("n", "vcc")]
+        u = [r for r in u if r != ("n", "vcc")] + ([("n", "vcc")] if args[-1] == "vcc" and len(args) > 4 else [])
     if _SCC_R.match(op):
         u = list(u) + [SCC]
     if _SCC_W.match(op):
@@ -141,9 +148,9 @@ def callee_writes(lines: list, funcs: list) -> dict:
         calls[name] = cs
         # restored by the function itself: whole-wave saved VGPRs, s30/s31 (return address), SP/FP/BP
         joined = "\n".join(txt)
-        for m in re.finditer(r"scratch_store_dword off, (v\d+), s3[23]( offset:\d+)?\s*; 4-byte Folded Spill\n"
+        for m in re.finditer(r"scratch_store_dword off, ([va]\d+), s3[23]( offset:\d+)?\s*; 4-byte Folded Spill\n"
                              r"\s*s_mov_b64 exec", joined):
-            ws.discard(("v", int(m.group(1)[1:])))
+            ws.discard((m.group(1)[0], int(m.group(1)[1:])))
         for r in (30, 31, 32, 33, 34):
             ws.discard(("s", r))
         w[name] = ws

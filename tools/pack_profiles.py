@@ -9,7 +9,9 @@ traffic figures were measured on the kernels it runs (`measured_at_head`).
                                                       #   the decode call   -> profiles/r06/pmc_decode_fused_8192.json
     python tools/pack_profiles.py tdec SUMMARY.json   # tdec_kbench --cts 100000 -> profiles/r06/pmc_tdec_100k.json
 
-Run it where the PMC passes ran (the GPU box), on the same tree.
+Run it where the PMC passes ran (the GPU box), on the same tree; OUT_ROOT
+(default the repo root) redirects the files, e.g. under gpurun_out/ so they
+come back from the box (then copy them into profiles/).
 """
 from __future__ import annotations
 
@@ -27,11 +29,12 @@ def main():
     s = json.load(open(summary))
     meta = {"csrc_sha16": source_digest(), "summary": os.path.relpath(summary, ROOT),
             "counters": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate rocprofv3 --pmc passes"}
-    os.makedirs(os.path.join(ROOT, "profiles", "r06"), exist_ok=True)
+    out_root = os.environ.get("OUT_ROOT", ROOT)
+    os.makedirs(os.path.join(out_root, "profiles", "r06"), exist_ok=True)
     if what == "rbc":
         enc = next(v for k, v in s.items() if k.startswith("rbc_encode_merkle<22, 42>"))
-        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        d = json.load(open(path))
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        path = os.path.join(out_root, "profiles", "pmc_traffic.json")
         rd, wr = enc["hbm_read_bytes_corrected"], enc["hbm_write_bytes"]
         d["rbc_encode_merkle_22_42"] = {
             "instances": 8192, "hbm_bytes_per_launch": rd + wr, "read": rd, "write": wr,
@@ -42,10 +45,10 @@ def main():
         json.dump(d, open(path, "w"), indent=1)
         dec = {k: v for k, v in s.items() if not k.startswith("rbc_encode_merkle")}
         dec["_meta"] = meta
-        json.dump(dec, open(os.path.join(ROOT, "profiles", "r06", "pmc_decode_fused_8192.json"), "w"), indent=1)
+        json.dump(dec, open(os.path.join(out_root, "profiles", "r06", "pmc_decode_fused_8192.json"), "w"), indent=1)
     elif what == "tdec":
         s["_meta"] = meta
-        json.dump(s, open(os.path.join(ROOT, "profiles", "r06", "pmc_tdec_100k.json"), "w"), indent=1)
+        json.dump(s, open(os.path.join(out_root, "profiles", "r06", "pmc_tdec_100k.json"), "w"), indent=1)
     else:
         raise SystemExit(f"unknown kind {what}")
     print("packed", what, meta["csrc_sha16"])
