@@ -90,6 +90,11 @@ typedef struct hbg_ctx hbg_ctx;
  * the engine runs one process per GPU (torch.distributed, RCCL over xGMI),
  * and instances are sharded across processes, never across the devices of
  * one context; a multi-device caller opens one context per device. */
+/* The first hbg_init of a process also runs a known-answer self-test of the
+ * BLS12-381 kernels (Ciphertext::verify and verify_decryption_share on a
+ * committed fixture, both kernel builds, per-share and batched schedules,
+ * ~tens of ms once); if any bit differs from the known answers, that and
+ * every later hbg_init of the process return HBG_E_DEVICE. */
 int hbg_init(hbg_ctx **out, int device);
 void hbg_free(hbg_ctx *ctx);
 int hbg_ctx_device(const hbg_ctx *ctx);  /* the device the context binds (< 0: ctx is NULL) */

@@ -92,3 +92,15 @@ def test_workload_generator_matches_oracle_statement():
     for inst in [0, 1, 77, 2 ** 33]:
         for n, e in [(64, 42), (16, 10), (4, 2), (128, 84)]:
             assert workload.erasure_mask(inst, n, e) == synth.erasure_mask(inst, n, e)
+
+
+def test_selftest_vectors_match_the_fixture(tmp_path):
+    """The power-on self-test's known answers (csrc/selftest_vectors.h,
+    api.hip run_self_test) are exactly what tools/gen_selftest_vectors.py
+    derives from the committed tests/golden/tdec_golden.json."""
+    import subprocess
+    import sys
+    out = tmp_path / "v.h"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_selftest_vectors.py"), "--out", str(out)],
+                   check=True, capture_output=True)
+    assert out.read_text() == open(os.path.join(ROOT, "hydrabadger_amd", "csrc", "selftest_vectors.h")).read()
