@@ -410,6 +410,15 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
     pts_ok = bool((st == 0).all().item()) and bool(torch.equal(pt, ep.msgs))
     ms = timed(run, reps)
     ms_v = timed(verify, reps)
+    # the deterministic schedule (hbg_set_share_verify(HBG_VERIFY_PER_SHARE): the
+    # crate's pairing equation per share) on the same shares: its time and bits
+    ctx.set_share_verify(_lib.HBG_VERIFY_PER_SHARE)
+    try:
+        ok.zero_()
+        ms_ps = timed(verify, 1)
+        ps_bits_ok = bool(np.array_equal(ok.cpu().numpy().astype(bool), ~ep.bad.reshape(-1)))
+    finally:
+        ctx.set_share_verify(_lib.HBG_VERIFY_BATCHED)
     kinds = {tw.BAD_KINDS[k]: int((ep.kind == k).sum()) for k in range(3)}
     out = {"metric": "TDec shares/s (ThresholdDecrypt: ct verify + verify_decryption_share + select + decrypt) "
                      "at N=64 t=21", "unit": "shares/s",
@@ -418,6 +427,17 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
            "n_ct": n_ct, "shares": n, "corrupted": int(ep.bad.sum()), "corrupted_by_kind": kinds,
            "faults_reported": int((oc == _lib.HBG_SHARE_FAULTY).sum().item()),
            "ok_bits_match": bits_ok, "outcomes_match": outcomes_ok, "plaintexts_match": pts_ok,
+           "batch_weights": {"bits": 127, "form": "a + b x^2, a odd, a and b the 64-bit halves of "
+                                                  "SHA3(K || batch digest || lane)",
+                             "key": "32 secret bytes from getrandom(2) at hbg_init",
+                             "soundness": "a (sub)batch check holding an invalid share passes with "
+                                          "probability <= 2^-127",
+                             "round5_threshold_decrypt_ms": 824.3,
+                             "round5_note": "32-bit public Fiat-Shamir halves (2^-63, grindable), BENCH_r05.json"},
+           "per_share_schedule": {"verify_ms": ms_ps, "verify_shares_per_s": n / (ms_ps * 1e-3),
+                                  "bits_match": ps_bits_ok,
+                                  "note": "hbg_set_share_verify(HBG_VERIFY_PER_SHARE): every bit the crate's own "
+                                          "pairing equation, deterministic"},
            "inputs": f"distinct: {n_ct} ciphertexts of 256-B contributions encrypted on the device under a seeded "
                      f"degree-{t} key set, all {N} decryption shares per ciphertext made on the device, "
                      f"{bad_rate:.0%} replaced (three kinds); generated in {t_gen:.1f} s, HBM-resident"}
@@ -913,6 +933,7 @@ def checks(decode, tdec, cfg1, n128, epoch, bwire, coin, wire) -> dict:
          "tdec_plaintexts_match": g(tdec, "cpu_baseline", "plaintexts_match"),
          "tdec_driver_outcomes_match": g(tdec, "outcomes_match"), "tdec_driver_bits_match": g(tdec, "ok_bits_match"),
          "tdec_driver_plaintexts_match": g(tdec, "plaintexts_match"),
+         "tdec_per_share_bits_match": g(tdec, "per_share_schedule", "bits_match"),
          "config1_roundtrip_ok": g(cfg1, "roundtrip_ok"), "n128_roundtrip_ok": g(n128, "roundtrip_ok"),
          "epoch_all_decrypted_ok": g(epoch, "all_decrypted_ok"), "broadcast_wire_roundtrip_ok": g(bwire, "roundtrip_ok"),
          "coin_all_ok": g(coin, "all_ok"), "wire_all_verified": g(wire, "all_verified")}
