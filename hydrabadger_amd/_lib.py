@@ -78,6 +78,7 @@ SIGNATURES = {
     "hbg_rs_reconstruct": (_i, [_vp, _u32, _u32, _u64, _u8p, _u64, _u8p, _vp, _u64, _u32]),
     "hbg_merkle_build": (_i, [_vp, _u32, _u64, _u8p, _u64, _u8p, _u64, _u32]),
     "hbg_merkle_validate": (_i, [_vp, _u32, _u64, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u8p, _u64, _u32]),
+    "hbg_merkle_validate_views": (_i, [_vp, _u32, _u64, _u8p, _u64, _vp, _u8p, _vp, _u8p, _u8p, _u64, _u32, _u32]),
     "hbg_rbc_encode_merkle": (_i, [_vp, _u32, _u8p, _u64, _vp, _u64, _u8p, _u64, _u8p, _u64, _u32]),
     "hbg_rbc_decode": (_i, [_vp, _u32, _u64, _u8p, _u64, _u8p, _u8p, _u8p, _u64, _vp, _u8p, _u64, _u32]),
     "hbg_proof_digests": (_u32, [_u32, _u32]),
@@ -106,6 +107,7 @@ SIGNATURES = {
     "hbg_test_set_rbc_fused": (_i, [_vp, C.c_int]),
     "hbg_test_set_rs_split": (_i, [_vp, C.c_int]),
     "hbg_test_set_rbc_decode_fused": (_i, [_vp, C.c_int]),
+    "hbg_test_set_merkle_pairs": (_i, [_vp, C.c_int]),
     "hbg_test_set_clock_probe": (_i, [_vp, _vp, C.c_uint64]),
     "hbg_test_set_latency_lanes": (C.c_uint64, [C.c_uint64]),
 }

@@ -67,6 +67,9 @@ struct hbg_ctx {
     // hbg_rbc_decode schedule (hbg_test_set_rbc_decode_fused): 0 plan -> coder(s) -> merkle_build, 1 / -1
     // (default) the fused rbc_decode_merkle where it exists ((D, Q) = (22, 42), N = 64)
     int dec_fused = -1;
+    // merkle_build's lane-pair blocks (hbg_test_set_merkle_pairs): -1 (default) for a
+    // partial last block generation, 0 never, 1 every block
+    int merkle_pairs = -1;
     // clock probe of the fused encoder (hbg_test_set_clock_probe): device buffer of clk_cap x 4 u64
     uint64_t* clk_buf = nullptr;
     uint64_t clk_cap = 0;
@@ -594,7 +597,7 @@ int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, 
     const uint32_t nodes = merkle_nodes(N);
     if (flags & HBG_DEVICE) {
         if (stride % 16 || !aligned(shards, 16) || !aligned(levels, 16)) return HBG_E_ARG;
-        HBG_TRY(launch_merkle_build(shards, stride, L, N, n, levels, c->stream));
+        HBG_TRY(launch_merkle_build(shards, stride, L, N, n, levels, c->stream, c->merkle_pairs));
         return finish(c, flags);
     }
     const uint64_t S = round_up(L, 16);
@@ -602,7 +605,7 @@ int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, 
     HBG_CHECK(scratch(c, 0, S * N * n, &d));
     HBG_CHECK(scratch(c, 3, (size_t)nodes * 32 * n, &dl));
     if (L) HBG_TRY(hipMemcpy2DAsync(d, S, shards, stride, L, N * n, hipMemcpyHostToDevice, c->stream));
-    HBG_TRY(launch_merkle_build((const uint8_t*)d, S, L, N, n, (uint8_t*)dl, c->stream));
+    HBG_TRY(launch_merkle_build((const uint8_t*)d, S, L, N, n, (uint8_t*)dl, c->stream, c->merkle_pairs));
     HBG_TRY(hipMemcpyAsync(levels, dl, (size_t)nodes * 32 * n, hipMemcpyDeviceToHost, c->stream));
     return sync_status(c);
 }
@@ -610,9 +613,17 @@ int hbg_merkle_build(hbg_ctx* c, uint32_t N, uint64_t L, const uint8_t* shards, 
 int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
                         const uint32_t* index, const uint8_t* digests, const uint32_t* ndig, const uint8_t* roots,
                         uint8_t* ok, uint64_t n, uint32_t flags) {
-    if (!c || N == 0 || N > 256 || vstride < len || (n && (!values || !index || !ndig || !roots || !ok)))
+    return hbg_merkle_validate_views(c, N, len, values, vstride, index, digests, ndig, roots, ok, n, 1, flags);
+}
+
+int hbg_merkle_validate_views(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
+                              const uint32_t* index, const uint8_t* digests, const uint32_t* ndig,
+                              const uint8_t* roots, uint8_t* ok, uint64_t n, uint32_t views, uint32_t flags) {
+    if (!c || N == 0 || N > 256 || vstride < len || views == 0 ||
+        (n && (!values || !index || !ndig || !roots || !ok)))
         return HBG_E_ARG;
     if (n == 0) return HBG_OK;
+    if (n > UINT64_MAX / views) return HBG_E_ARG;
     CtxLock g(c);
     HBG_TRY(hipSetDevice(c->device));
     const uint32_t depth = merkle_depth(N);
@@ -620,7 +631,7 @@ int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* val
     if (flags & HBG_DEVICE) {
         if (vstride % 16 || !aligned(values, 16)) return HBG_E_ARG;
         HBG_TRY(launch_merkle_validate(N, len, values, vstride, index, digests, depth, ndig, roots, ok, n,
-                                       c->stream));
+                                       c->stream, views));
         return finish(c, flags);
     }
     const uint64_t S = round_up(len ? len : 1, 16);
@@ -630,15 +641,15 @@ int hbg_merkle_validate(hbg_ctx* c, uint32_t N, uint64_t len, const uint8_t* val
     HBG_CHECK(scratch(c, 2, (size_t)32 * depth * n + 16, &dd));
     HBG_CHECK(scratch(c, 4, 4 * n, &dn));
     HBG_CHECK(scratch(c, 5, 32 * n, &dr));
-    HBG_CHECK(scratch(c, 6, n, &dok));
+    HBG_CHECK(scratch(c, 6, n * views, &dok));
     if (len) HBG_TRY(hipMemcpy2DAsync(dv, S, values, vstride, len, n, hipMemcpyHostToDevice, c->stream));
     HBG_TRY(hipMemcpyAsync(di, index, 4 * n, hipMemcpyHostToDevice, c->stream));
     if (depth) HBG_TRY(hipMemcpyAsync(dd, digests, (size_t)32 * depth * n, hipMemcpyHostToDevice, c->stream));
     HBG_TRY(hipMemcpyAsync(dn, ndig, 4 * n, hipMemcpyHostToDevice, c->stream));
     HBG_TRY(hipMemcpyAsync(dr, roots, 32 * n, hipMemcpyHostToDevice, c->stream));
     HBG_TRY(launch_merkle_validate(N, len, (const uint8_t*)dv, S, (const uint32_t*)di, (const uint8_t*)dd, depth,
-                                   (const uint32_t*)dn, (const uint8_t*)dr, (uint8_t*)dok, n, c->stream));
-    HBG_TRY(hipMemcpyAsync(ok, dok, n, hipMemcpyDeviceToHost, c->stream));
+                                   (const uint32_t*)dn, (const uint8_t*)dr, (uint8_t*)dok, n, c->stream, views));
+    HBG_TRY(hipMemcpyAsync(ok, dok, n * views, hipMemcpyDeviceToHost, c->stream));
     return sync_status(c);
 }
 
@@ -666,7 +677,7 @@ int hbg_rbc_encode_merkle(hbg_ctx* c, uint32_t N, const uint8_t* payloads, uint6
         } else {
             HBG_TRY(launch_pack_rows(dsh, S, L, N, N, n, dpay, dps, dplen, c->stream));
         }
-        HBG_TRY(launch_merkle_build(dsh, S, L, N, n, dlev, c->stream));
+        HBG_TRY(launch_merkle_build(dsh, S, L, N, n, dlev, c->stream, c->merkle_pairs));
         return HBG_OK;
     };
     if (flags & HBG_DEVICE) {
@@ -721,7 +732,7 @@ int hbg_rbc_decode(hbg_ctx* c, uint32_t N, uint64_t L, uint8_t* shards, uint64_t
                 // Trivial coding: every shard must be present (hbbft Coding::reconstruct_shards)
                 HBG_TRY(launch_rbc_trivial_status(n, N, dpres, (int32_t*)ds, c->stream));
             }
-            HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream));
+            HBG_TRY(launch_merkle_build(dsh, S, L, N, n, (uint8_t*)dl, c->stream, c->merkle_pairs));
         }
         HBG_TRY(launch_rbc_glue(dsh, S, L, N, D, n, (const uint8_t*)dl, droots, (const int32_t*)ds, dplen, dstat, dout,
                                 dos, c->stream, !fused));
@@ -1542,6 +1553,13 @@ int hbg_test_set_rs_split(hbg_ctx* c, int on) {
     if (!c || on < -1 || on > 1) return HBG_E_ARG;
     CtxLock g(c);
     c->rs_split = on;
+    return HBG_OK;
+}
+
+int hbg_test_set_merkle_pairs(hbg_ctx* c, int on) {
+    if (!c || on < -1 || on > 1) return HBG_E_ARG;
+    CtxLock g(c);
+    c->merkle_pairs = on;
     return HBG_OK;
 }
 

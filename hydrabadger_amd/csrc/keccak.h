@@ -216,4 +216,134 @@ __device__ __forceinline__ void sha3_256_aligned8(const uint8_t* __restrict__ p,
     }
 }
 
+// ---- two-lane sponge: one Keccak state on a lane pair (2k, 2k + 1) -------
+// Lane half h = lane & 1 holds the h-th 32-bit half of every 64-bit word, so a
+// state is 25 VGPRs a lane.  A 64-bit rotation needs the partner's half (one
+// DPP quad_perm [1,0,3,2] move) and one v_alignbit — the same instruction for
+// both halves.  Per round and lane: 120 VALU (29 v_alignbit) against the
+// one-lane round's 180 (58): a wave of 32 sponges takes ~0.63 of the time of a
+// wave of 64, so merkle_build runs a launch's partial last wave generation
+// this way (more waves, each shorter: launch_merkle_build).
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1, 0, 3, 2]
+}
+
+// the own half of rotl64(w, N), given the own half of w
+template <int N>
+__device__ __forceinline__ uint32_t rotl_half(uint32_t own) {
+    if constexpr (N == 0) {
+        return own;
+    } else {
+        const uint32_t p = pair_swap(own);
+        if constexpr (N == 32) return p;
+        else if constexpr (N < 32) return __builtin_amdgcn_alignbit(own, p, 32 - N);
+        else return __builtin_amdgcn_alignbit(p, own, 64 - N);
+    }
+}
+
+#define HBG_THETA_RHO_HALF(x, y, r, dst) \
+    b[dst] = rotl_half<r>(xor3(a[(x) + 5 * (y)], C[((x) + 4) % 5], E[((x) + 1) % 5]));
+
+__device__ __forceinline__ void keccak_round_half(uint32_t (&a)[25], uint32_t rc) {
+    uint32_t C[5], E[5], b[25];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) C[x] = xor3(xor3(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
+#pragma unroll
+    for (int x = 0; x < 5; ++x) E[x] = rotl_half<1>(C[x]);
+    HBG_THETA_RHO_HALF(0, 0, 0, 0)
+    HBG_THETA_RHO_HALF(1, 0, 1, 10)
+    HBG_THETA_RHO_HALF(2, 0, 62, 20)
+    HBG_THETA_RHO_HALF(3, 0, 28, 5)
+    HBG_THETA_RHO_HALF(4, 0, 27, 15)
+    HBG_THETA_RHO_HALF(0, 1, 36, 16)
+    HBG_THETA_RHO_HALF(1, 1, 44, 1)
+    HBG_THETA_RHO_HALF(2, 1, 6, 11)
+    HBG_THETA_RHO_HALF(3, 1, 55, 21)
+    HBG_THETA_RHO_HALF(4, 1, 20, 6)
+    HBG_THETA_RHO_HALF(0, 2, 3, 7)
+    HBG_THETA_RHO_HALF(1, 2, 10, 17)
+    HBG_THETA_RHO_HALF(2, 2, 43, 2)
+    HBG_THETA_RHO_HALF(3, 2, 25, 12)
+    HBG_THETA_RHO_HALF(4, 2, 39, 22)
+    HBG_THETA_RHO_HALF(0, 3, 41, 23)
+    HBG_THETA_RHO_HALF(1, 3, 45, 8)
+    HBG_THETA_RHO_HALF(2, 3, 15, 18)
+    HBG_THETA_RHO_HALF(3, 3, 21, 3)
+    HBG_THETA_RHO_HALF(4, 3, 8, 13)
+    HBG_THETA_RHO_HALF(0, 4, 18, 14)
+    HBG_THETA_RHO_HALF(1, 4, 2, 24)
+    HBG_THETA_RHO_HALF(2, 4, 61, 9)
+    HBG_THETA_RHO_HALF(3, 4, 56, 19)
+    HBG_THETA_RHO_HALF(4, 4, 14, 4)
+#pragma unroll
+    for (int y = 0; y < 5; ++y) {
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+            a[x + 5 * y] = b[x + 5 * y] ^ (~b[(x + 1) % 5 + 5 * y] & b[(x + 2) % 5 + 5 * y]);
+    }
+    a[0] ^= rc;
+}
+#undef HBG_THETA_RHO_HALF
+
+__device__ __forceinline__ void keccak_f_half(uint32_t (&a)[25], uint32_t half) {
+#pragma unroll 2
+    for (int r = 0; r < 24; ++r) keccak_round_half(a, half ? kKeccakRC[2 * r + 1] : kKeccakRC[2 * r]);
+}
+
+// SHA3-256 of `len` bytes at an 8-byte-aligned device address by a lane pair:
+// both lanes pass the same p and len, half = lane & 1; out = this lane's halves
+// of the digest's four 64-bit words (digest word 2i + half).  Every lane of the
+// wave runs the permutations (the DPP moves read the partner lane): pairs
+// without a sponge pass len = 0 and discard the result.  Reads as
+// sha3_256_aligned8.
+template <bool PREFETCH = false>
+__device__ __forceinline__ void sha3_256_aligned8_pair(const uint8_t* __restrict__ p, uint64_t len, uint32_t half,
+                                                       uint32_t (&out)[4]) {
+    uint32_t a[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) a[i] = 0u;
+    const uint64_t nfull = len / 136;
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p) + half;
+    uint32_t w[17];
+    if (PREFETCH && nfull) {
+#pragma unroll
+        for (int i = 0; i < 17; ++i) w[i] = q[2 * i];
+    }
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
+        if (!PREFETCH) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w[i] = q[2 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < 17; ++i) a[i] ^= w[i];
+        q += 34;
+        if (PREFETCH && blk + 1 < nfull) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) w[i] = q[2 * i];
+        }
+        keccak_f_half(a, half);
+    }
+    const uint32_t rem = (uint32_t)(len - nfull * 136);
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        const int32_t left = (int32_t)rem - (int32_t)(8 * i + 4 * half);  // message bytes in this half-word
+        if (left > 0) {
+            uint32_t v = q[2 * i];
+            if (left < 4) v &= (1u << (8 * left)) - 1u;
+            a[i] ^= v;
+        }
+    }
+    {
+        const uint32_t wi = rem >> 3, sh = (rem & 7) * 8;
+        const uint32_t hh = sh < 32 ? 0u : 1u;
+#pragma unroll
+        for (int i = 0; i < 17; ++i)
+            if ((uint32_t)i == wi && hh == half) a[i] ^= 0x06u << (sh & 31u);
+        if (half) a[16] ^= 0x80000000u;
+    }
+    keccak_f_half(a, half);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = a[i];
+}
+
 }  // namespace hbg

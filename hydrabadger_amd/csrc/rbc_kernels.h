@@ -113,12 +113,14 @@ bool has_fused_decoder(uint32_t D, uint32_t Q);
 hipError_t launch_rbc_decode_merkle(uint32_t D, uint32_t Q, uint8_t* shards, uint64_t S, uint64_t L, uint64_t n,
                                     const uint8_t* present, const uint8_t* plans, uint64_t plan_stride,
                                     uint8_t* levels, uint8_t* out, uint64_t ostride, hipStream_t st);
+// split: -1 lane-pair blocks for a partial last generation (<= half the CUs),
+// 0 one-lane blocks only, 1 lane-pair blocks only (hbg_test_set_merkle_pairs)
 hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
-                               uint8_t* levels, hipStream_t st);
+                               uint8_t* levels, hipStream_t st, int split = -1);
 hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
                                   const uint32_t* index, const uint8_t* digests, uint32_t depth,
                                   const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
-                                  hipStream_t st);
+                                  hipStream_t st, uint32_t views = 1);  // ok: [views][n], every view validates all n
 hipError_t launch_rbc_glue(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint32_t D, uint64_t n,
                            const uint8_t* levels, const uint8_t* roots, const int32_t* rstatus, uint64_t* plen,
                            uint8_t* status, uint8_t* out, uint64_t ostride, hipStream_t st, bool copy = true);

@@ -533,17 +533,37 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
 // ============================================================== family 2: Merkle
 // One work-item per leaf; lanes_per_inst = next_pow2(N) (<= 256); tree levels
 // built in LDS by the owning lanes.  levels: [n][nodes][32].
+// Blocks from b1 on (instances from n1 on) hash each leaf on a lane PAIR
+// (sha3_256_aligned8_pair, 2 * lpi lanes an instance): launch_merkle_build
+// sends the launch's partial last generation of blocks there, as twice the
+// blocks of ~0.63 the duration, so it spreads over every CU instead of
+// adding a whole block duration on some of them.
 __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                     uint32_t N, uint32_t lpi, uint32_t nodes, uint64_t n,
-                                                    uint8_t* __restrict__ levels) {
+                                                    uint8_t* __restrict__ levels, uint32_t b1, uint64_t n1) {
     extern __shared__ __attribute__((aligned(16))) uint32_t mlds[];
-    const uint32_t ipb = 256 / lpi;
-    const uint32_t li = threadIdx.x / lpi, leaf = threadIdx.x % lpi;
-    const uint64_t inst = (uint64_t)blockIdx.x * ipb + li;
+    const bool pair = blockIdx.x >= b1;
+    const uint32_t lanes = pair ? 2 * lpi : lpi;       // lanes per instance
+    const uint32_t li = threadIdx.x / lanes, tl = threadIdx.x % lanes;
+    const uint64_t inst = pair ? n1 + (uint64_t)(blockIdx.x - b1) * (256 / lanes) + li
+                               : (uint64_t)blockIdx.x * (256 / lpi) + li;
     const bool live = inst < n;
     uint32_t* tree = mlds + (uint64_t)li * nodes * 8;
     uint4* gout = reinterpret_cast<uint4*>(levels + inst * (uint64_t)nodes * 32);
-    if (live && leaf < N) {
+    if (pair) {
+        const uint32_t leaf = tl >> 1, half = tl & 1u;
+        if (live && leaf < N) {
+            uint32_t d[4];
+            sha3_256_aligned8_pair<true>(shards + (inst * N + leaf) * S, L, half, d);
+            uint32_t* g = reinterpret_cast<uint32_t*>(gout) + leaf * 8 + half;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                tree[leaf * 8 + 2 * i + half] = d[i];
+                g[2 * i] = d[i];
+            }
+        }
+    } else if (live && tl < N) {
+        const uint32_t leaf = tl;
         uint32_t d[8];
         sha3_256_aligned8<1, true>(shards + (inst * N + leaf) * S, L, d);
 #pragma unroll
@@ -552,6 +572,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
         gout[2 * leaf + 1] = make_uint4(d[4], d[5], d[6], d[7]);
     }
     __syncthreads();
+    const uint32_t leaf = tl;  // the tree levels: one lane a node
     uint32_t base = 0, cnt = N;
     while (cnt > 1) {
         const uint32_t nn = (cnt + 1) / 2;
@@ -1227,15 +1248,19 @@ void rbc_decode_merkle(uint8_t* __restrict__ shards, uint64_t S, uint64_t L, uin
     }
 }
 
-// Proof::validate(N) — one work-item per proof.
+// Proof::validate(N) — one work-item per proof.  Work-item q validates proof
+// k = q % n_base of the table (n_base = n: every proof once; n = views *
+// n_base: each view's own validation of the whole table, ok view-major —
+// hbg_merkle_validate_views), so views need no copies of the table.
 __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len, const uint8_t* __restrict__ values,
                                                        uint64_t vstride, const uint32_t* __restrict__ index,
                                                        const uint8_t* __restrict__ digests, uint32_t depth,
                                                        const uint32_t* __restrict__ ndig,
                                                        const uint8_t* __restrict__ roots, uint8_t* __restrict__ ok,
-                                                       uint64_t n) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
+                                                       uint64_t n, uint64_t n_base) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const uint64_t k = q < n_base ? q : q % n_base;
     uint32_t d[8];
     sha3_256_aligned8<1>(values + k * vstride, len, d);
     uint32_t li = index[k], ln = N, used = 0;
@@ -1264,7 +1289,7 @@ __global__ __launch_bounds__(256) void merkle_validate(uint32_t N, uint64_t len,
 #pragma unroll
         for (int i = 0; i < 8; ++i) good &= (rt[i] == d[i]);
     }
-    ok[k] = good ? 1 : 0;
+    ok[q] = good ? 1 : 0;
 }
 
 // ============================================================== glue (a8)
@@ -1513,26 +1538,57 @@ hipError_t launch_rs_plan(const uint8_t* present, uint32_t D, uint32_t Q, uint32
     return hipGetLastError();
 }
 
+// Compute units of the current device (the partial-generation split below).
+static uint32_t device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return 0;
+    return (uint32_t)cus;
+}
+
+// The blocks past the last whole generation (one block a CU) — when they
+// would fill at most half of the CUs — hash on lane pairs instead: twice the
+// blocks, each ~0.63 of a block's duration, one a CU.  configs[1] (N = 16,
+// 10 k instances: 625 blocks on 256 CUs): 2 + 0.63 block durations instead of
+// 3.  Whole generations (the headline shapes, the epoch's chunks) are
+// unchanged.  split = 0: one-lane blocks only, 1: lane pairs only (tests).
 hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, uint32_t N, uint64_t n,
-                               uint8_t* levels, hipStream_t st) {
+                               uint8_t* levels, hipStream_t st, int split) {
     uint32_t lpi = 1;
     while (lpi < N) lpi <<= 1;
     const uint32_t nodes = merkle_nodes(N);
     const uint32_t ipb = 256 / lpi;
     const uint64_t blocks = (n + ipb - 1) / ipb;
+    uint64_t b1 = blocks, b2 = 0;
+    if (lpi <= 128 && split != 0) {
+        const uint32_t cus = device_cus();
+        const uint64_t gen = cus ? blocks / cus * cus : blocks;  // blocks in whole generations
+        const uint64_t tail = n - std::min<uint64_t>(n, gen * ipb), tb = (tail + ipb / 2 - 1) / (ipb / 2);
+        if (split == 1) {
+            b1 = 0;
+            b2 = (n + ipb / 2 - 1) / (ipb / 2);
+        } else if (cus && tail && tb <= cus) {
+            b1 = gen;
+            b2 = tb;
+        }
+    }
     const size_t lds = (size_t)ipb * nodes * 32;
-    HBG_GRID_CHECK(blocks, 256);
-    merkle_build<<<dim3((uint32_t)blocks), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels);
+    HBG_GRID_CHECK(b1 + b2, 256);
+    merkle_build<<<dim3((uint32_t)(b1 + b2)), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels,
+                                                                   (uint32_t)b1, b1 * ipb);
     return hipGetLastError();
 }
 
 hipError_t launch_merkle_validate(uint32_t N, uint64_t len, const uint8_t* values, uint64_t vstride,
                                   const uint32_t* index, const uint8_t* digests, uint32_t depth,
                                   const uint32_t* ndig, const uint8_t* roots, uint8_t* ok, uint64_t n,
-                                  hipStream_t st) {
-    HBG_GRID_CHECK((n + 255) / 256, 256);
-    merkle_validate<<<dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index, digests,
-                                                                           depth, ndig, roots, ok, n);
+                                  hipStream_t st, uint32_t views) {
+    const uint64_t total = n * views;
+    HBG_GRID_CHECK((total + 255) / 256, 256);
+    merkle_validate<<<dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st>>>(N, len, values, vstride, index,
+                                                                               digests, depth, ndig, roots, ok, total,
+                                                                               n);
     return hipGetLastError();
 }
 

@@ -108,6 +108,56 @@ def _copies(x: torch.Tensor, c: int) -> torch.Tensor:
     return x.repeat(*reps)
 
 
+class _CopyPipe:
+    """Every decode chunk's views get their own copy of the shard table (the
+    decoder reconstructs in place).  On a GPU the copies of chunk i + 1 are
+    made on a side stream while chunk i decodes (two buffers: chunk i + 2's
+    copy waits for chunk i's decode); elsewhere they are made on demand."""
+
+    def __init__(self, x: torch.Tensor, chunks, dev):
+        self.x, self.chunks = x, chunks
+        self.gpu = dev.type == "cuda" and len(chunks) > 1
+        if not self.gpu:
+            return
+        self.main = torch.cuda.current_stream(dev)
+        self.side = torch.cuda.Stream(dev)
+        cmax = max(c for _, c in chunks)
+        self.bufs = [torch.empty((cmax,) + tuple(x.shape), dtype=x.dtype, device=dev) for _ in range(2)]
+        self.copied, self.decoded = {}, {}
+        self.side.wait_stream(self.main)   # x is written on the main stream
+        self._copy(0)
+
+    def _copy(self, i: int):
+        c = self.chunks[i][1]
+        with torch.cuda.stream(self.side):
+            if i >= 2:
+                self.side.wait_event(self.decoded[i - 2])
+            dst = self.bufs[i % 2][:c]
+            src = self.x.unsqueeze(0).expand((c,) + tuple(self.x.shape))
+            if self.x.dtype == torch.uint8 and self.x.shape[-1] % 8 == 0 and self.x.is_contiguous():
+                dst, src = dst.view(torch.int64), self.x.view(torch.int64).unsqueeze(0).expand((c,) + tuple(
+                    self.x.view(torch.int64).shape))
+            dst.copy_(src)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            self.copied[i] = ev
+
+    def get(self, i: int) -> torch.Tensor:
+        c = self.chunks[i][1]
+        if not self.gpu:
+            return _copies(self.x, c)
+        if i + 1 < len(self.chunks):
+            self._copy(i + 1)
+        self.main.wait_event(self.copied[i])
+        return self.bufs[i % 2][:c].reshape((c * self.x.shape[0],) + tuple(self.x.shape[1:]))
+
+    def done(self, i: int):
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record(self.main)
+            self.decoded[i] = ev
+
+
 def arrival_orders(epoch: int, proposers, n: int, node: int = -1) -> np.ndarray:
     """[k][n] senders of instance proposers[k]'s decryption shares in arrival
     order at `node` (-1: the shared view) — a seeded permutation: the
@@ -263,13 +313,13 @@ class HoneyBadgerEpoch:
         return value_ok, vrecv, run_off, len(g_len)
 
     def run(self, epoch: int = 0, faults: Faults = Faults(), per_node: bool = True,
-            decode_chunk: int = 32, echo_chunk: int = 32) -> EpochResult:
+            decode_chunk: int = 32) -> EpochResult:
         """One epoch.  per_node: every local node does its own work (Values
         addressed to it, all echoes, its decodes, its ThresholdDecrypt of every
         accepted ciphertext with its own arrival order); otherwise the shared
         view (one check / decode / TDec instance per rank on behalf of all
-        its nodes).  decode_chunk / echo_chunk: local nodes whose decode
-        copies / echo tables are resident (and launched) at once."""
+        its nodes).  decode_chunk: local nodes whose decode copies are
+        resident (and launched) at once (the decoder reconstructs in place)."""
         e, N, m, L, C, P, f = self.engine, self.N, self.m, self.L, self.C, self.P, self.f
         dev = e.device
         r0 = self.rank * m
@@ -335,14 +385,10 @@ class HoneyBadgerEpoch:
         s_of = torch.arange(N, dtype=torch.int32, device=dev).repeat_interleave(N)
         parsed = (st == 0) & (tag == _lib.HBG_MSG_ECHO) & (idx == s_of)
         # every view validates every echo it receives (hbbft handle_echo): each
-        # view its own copy of the N x N echoes, up to echo_chunk views per
-        # launch (one view's N*N proofs are too few lanes to fill the chip)
-        eok = []
-        for c0 in range(0, nv, echo_chunk):
-            c = min(echo_chunk, nv - c0)
-            rep = (lambda x: _copies(x, c))
-            okc = e.validate_table(N, L, rep(vals), rep(idx), rep(dig), rep(nd), rep(roots))
-            eok += list(okc.view(c, -1))
+        # view hashes the N x N echoes itself, all views in one launch over the
+        # one parsed table (hbg_merkle_validate_views: one view's N*N proofs
+        # are too few lanes to fill the chip; no per-view copies)
+        eok = list(e.validate_table(N, L, vals, idx, dig, nd, roots, views=nv).view(nv, -1))
         work["echo_validations"] = nv * N * N
         echo_ok_v = torch.stack([(parsed & (x == 1)).view(N, N) & (esent_all == 1) for x in eok])   # [v][s][p]
         # echoes per root: the root with the most valid echoes (ties: lowest sender)
@@ -385,11 +431,13 @@ class HoneyBadgerEpoch:
         OS = (D * L + 15) // 16 * 16
         out = e.zeros((nv, N, OS))                            # every view's decodes, written in place
         plens, dsts = [], []
-        for c0 in range(0, nv, decode_chunk):
-            c = min(decode_chunk, nv - c0)
-            _, pl, ds = e.decode(N, L, _copies(sh, c), present[c0:c0 + c].reshape(c * N, N).contiguous(),
+        chunks = [(c0, min(decode_chunk, nv - c0)) for c0 in range(0, nv, decode_chunk)]
+        copies = _CopyPipe(sh, chunks, dev)   # chunk i+1's copies made beside chunk i's decode
+        for i, (c0, c) in enumerate(chunks):
+            _, pl, ds = e.decode(N, L, copies.get(i), present[c0:c0 + c].reshape(c * N, N).contiguous(),
                                  root_p[c0:c0 + c].reshape(c * N, 32).contiguous(),
                                  out=out[c0:c0 + c].view(c * N, OS))
+            copies.done(i)
             plens.append(pl.view(c, N))
             dsts.append(ds.view(c, N))
         plen, dst = torch.cat(plens), torch.cat(dsts)          # [v][p]

@@ -215,12 +215,15 @@ class DeviceEngine:
                            st, ctx=self.ctx, device=True, asynchronous=True)
         return tag, vals, index, dig, nd, roots, st
 
-    def validate_table(self, n_nodes: int, L: int, vals, index, dig, nd, roots):
+    def validate_table(self, n_nodes: int, L: int, vals, index, dig, nd, roots, views: int = 1):
+        """Proof::validate of every row; with views > 1 each of `views` nodes
+        validates the whole table itself (ok [views * rows], view-major)."""
         M = vals.shape[0]
-        ok = self.zeros((M,))
-        _lib.check(_lib.lib().hbg_merkle_validate(self.ctx.h, n_nodes, L, vals.data_ptr(), vals.shape[-1],
-                                                  index.data_ptr(), dig.data_ptr(), nd.data_ptr(), roots.data_ptr(),
-                                                  ok.data_ptr(), M, self._flags()), "Proof::validate")
+        ok = self.zeros((M * views,))
+        _lib.check(_lib.lib().hbg_merkle_validate_views(self.ctx.h, n_nodes, L, vals.data_ptr(), vals.shape[-1],
+                                                        index.data_ptr(), dig.data_ptr(), nd.data_ptr(),
+                                                        roots.data_ptr(), ok.data_ptr(), M, views, self._flags()),
+                   "Proof::validate")
         return ok
 
     def decrypt_shares(self, U48, sk32, pair_ct, pair_sk):

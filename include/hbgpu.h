@@ -151,6 +151,16 @@ int hbg_merkle_validate(hbg_ctx *ctx, uint32_t N, uint64_t value_len, const uint
                         const uint32_t *ndigests, const uint8_t *roots, uint8_t *ok,
                         uint64_t n_proofs, uint32_t flags);
 
+/* The same n_proofs proofs validated by each of n_views nodes on its own
+ * (hbbft handle_echo at every node: the N^3 of an epoch):
+ * ok[v * n_proofs + k] is view v's Proof::validate of proof k.  Every view
+ * hashes the proofs itself; the views read one table (no per-view copies).
+ * n_views = 1 is hbg_merkle_validate. */
+int hbg_merkle_validate_views(hbg_ctx *ctx, uint32_t N, uint64_t value_len, const uint8_t *values,
+                              uint64_t value_stride, const uint32_t *index, const uint8_t *digests,
+                              const uint32_t *ndigests, const uint8_t *roots, uint8_t *ok,
+                              uint64_t n_proofs, uint32_t n_views, uint32_t flags);
+
 /* Broadcast::send_shards fused (a2+a3+a4): payload k (payload_len[k] bytes at
  * payloads + k*payload_stride) -> BE u32 length prefix, zero pad, chunk into N
  * shards of shard_len, RS-encode, Merkle-tree.  Every payload_len[k] must give

@@ -40,6 +40,13 @@ int hbg_test_set_rs_split(hbg_ctx *ctx, int on);
  * (D, Q) = (22, 42), N = 64 — and the three-launch schedule elsewhere.
  * Identical shards, levels, statuses and payloads. */
 int hbg_test_set_rbc_decode_fused(hbg_ctx *ctx, int on);
+/* Choose merkle_build's leaf hashing (hbg_merkle_build, the two-launch
+ * hbg_rbc_encode_merkle / hbg_rbc_decode schedules): 0 one lane a leaf; 1 a
+ * lane pair a leaf (each lane half of every Keccak word) in every block; -1
+ * (the default) lane pairs for the blocks past the launch's last whole
+ * generation (one block a CU) when they would fill at most half the CUs, one
+ * lane elsewhere.  Identical levels. */
+int hbg_test_set_merkle_pairs(hbg_ctx *ctx, int on);
 /* Clock probe of the fused send_shards kernel (rbc_encode_merkle): while set,
  * every hbg_rbc_encode_merkle launch of at most cap_workgroups workgroups
  * (one per instance at N = 64) writes 4 u64 per workgroup to dev_buf

@@ -87,6 +87,10 @@ extern "C" {
                                value_stride: u64, index: *const u32, digests: *const u8,
                                ndigests: *const u32, roots: *const u8, ok: *mut u8, n_proofs: u64,
                                flags: u32) -> c_int;
+    pub fn hbg_merkle_validate_views(ctx: *mut hbg_ctx, n_nodes: u32, value_len: u64, values: *const u8,
+                                     value_stride: u64, index: *const u32, digests: *const u8,
+                                     ndigests: *const u32, roots: *const u8, ok: *mut u8, n_proofs: u64,
+                                     n_views: u32, flags: u32) -> c_int;
     pub fn hbg_rbc_encode_merkle(ctx: *mut hbg_ctx, n_nodes: u32, payloads: *const u8, payload_stride: u64,
                                  payload_len: *const u64, shard_len: u64, shards: *mut u8, shard_stride: u64,
                                  levels: *mut u8, n: u64, flags: u32) -> c_int;

@@ -97,7 +97,9 @@ class OracleEngine:
         return (i32(tag), torch.from_numpy(vals), i32(index), torch.from_numpy(dig), i32(nd), torch.from_numpy(roots),
                 torch.from_numpy(st.astype(np.int32)))
 
-    def validate_table(self, N, L, vals, index, dig, nd, roots):
+    def validate_table(self, N, L, vals, index, dig, nd, roots, views=1):
+        if views > 1:  # every view validates the table itself
+            return torch.cat([self.validate_table(N, L, vals, index, dig, nd, roots) for _ in range(views)])
         ok = np.zeros(vals.shape[0], np.uint8)
         for q in range(vals.shape[0]):
             k = int(nd[q]) & 0xFFFFFFFF

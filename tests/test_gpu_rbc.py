@@ -390,6 +390,42 @@ def test_fused_schedule_matches_two_launch_schedule(N, P, n):
         assert np.array_equal(out[1][1][k], rl), k
 
 
+@pytest.mark.parametrize("N,L,n", [(16, 10924, 10000), (16, 10924, 21), (5, 137, 700), (64, 16384, 7),
+                                   (128, 135, 300), (100, 1000, 77), (1, 7, 50), (2, 272, 33), (7, 0, 9),
+                                   (16, 136, 4100), (128, 8, 1000)])
+def test_merkle_pairs_schedule_matches(N, L, n):
+    """hbg_test_set_merkle_pairs: merkle_build hashing every leaf on a lane pair
+    (1), on one lane (0) and the default split (-1: lane pairs for a partial
+    last block generation — configs[1]'s 10,000 x 16 leaves included) write
+    identical levels, and they match the oracle's tree on sampled instances
+    (block-boundary lengths: 0, 7, 8, 135, 136, 137, 272)."""
+    torch = _torch()
+    from hydrabadger_amd import _lib
+    S = max(16, (L + 15) // 16 * 16)
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(N * 131 + L * 7 + n)
+    shards = torch.randint(0, 256, (n, N, S), dtype=torch.uint8, generator=g).to(dev)
+    nodes = _lib.merkle_nodes(N)
+    out = []
+    ctx = _lib.Context(0)
+    try:
+        for mode in (0, 1, -1):
+            _lib.check(_lib.lib().hbg_test_set_merkle_pairs(ctx.h, mode))
+            levels = torch.full((n, nodes, 32), 0x5A, dtype=torch.uint8, device=dev)
+            _lib.check(_lib.lib().hbg_merkle_build(ctx.h, N, L, shards.data_ptr(), S, levels.data_ptr(), n,
+                                                   _lib.HBG_DEVICE))
+            torch.cuda.synchronize()
+            out.append(levels.cpu().numpy())
+        assert _lib.lib().hbg_test_set_merkle_pairs(ctx.h, 2) == _lib.HBG_E_ARG
+    finally:
+        ctx.close()
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[0], out[2])
+    host = shards.cpu().numpy()
+    for k in sorted({0, n // 2, n - 1}):
+        ref = merkle.MerkleTree.from_vec([host[k, i, :L].tobytes() for i in range(N)])
+        assert [out[1][k, j].tobytes() for j in range(nodes)] == ref.flat_levels(), k
+
+
 @pytest.mark.parametrize("D,Q", [(2, 2), (6, 10), (22, 42), (44, 84)])
 @pytest.mark.parametrize("L", [1, 5, 257, 4099])
 def test_reconstruct_split_schedule_matches_one_pass(D, Q, L):

@@ -164,6 +164,13 @@ def test_gpu_read_table_fields_for_bad_layouts():
     assert lib().hbg_merkle_validate(default_context().h, N, L, ptr(vals), L, ptr(index), ptr(dig), ptr(nd),
                                      ptr(roots), ptr(ok), m, 0) == 0
     assert list(ok[1:]) == [0, 1]
+    # each of three views validates the table itself (host mode), view-major
+    ok3 = np.full(3 * m, 7, np.uint8)
+    assert lib().hbg_merkle_validate_views(default_context().h, N, L, ptr(vals), L, ptr(index), ptr(dig), ptr(nd),
+                                           ptr(roots), ptr(ok3), m, 3, 0) == 0
+    assert np.array_equal(ok3, np.tile(ok, 3))
+    assert lib().hbg_merkle_validate_views(default_context().h, N, L, ptr(vals), L, ptr(index), ptr(dig), ptr(nd),
+                                           ptr(roots), ptr(ok3), m, 0, 0) == _lib.HBG_E_ARG
 
 
 def _torch():
@@ -235,6 +242,14 @@ def test_gpu_device_batch_write_read_validate(N, P, n):
     expect = np.ones(m, np.uint8)
     expect[bad] = 0
     assert np.array_equal(ok.cpu().numpy(), expect)
+    # every view of a rank validates the whole table itself, one launch, no copies
+    views = 5
+    okv = torch.full((views * m,), 7, dtype=torch.uint8, device=dev)
+    assert _lib.lib().hbg_merkle_validate_views(h, N, L, _lib.ptr(vals), S, _lib.ptr(rindex), _lib.ptr(dig),
+                                                _lib.ptr(nd), _lib.ptr(roots), _lib.ptr(okv), m, views,
+                                                _lib.HBG_DEVICE) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(okv.cpu().numpy(), np.tile(expect, views))
     good = np.setdiff1d(np.arange(m), bad)
     ref_vals = shards.reshape(m, S)[:, :L]
     assert torch.equal(vals[torch.from_numpy(good).to(dev), :L], ref_vals[torch.from_numpy(good).to(dev)])

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--splits", default="0,1",
                     help="decode schedules to time (hbg_test_set_rs_split): 0 one-pass, 1 data rows + constant "
                          "parity encoder, -1 the library default")
+    ap.add_argument("--pairs", default="-1",
+                    help="merkle_build leaf schedules to time (hbg_test_set_merkle_pairs): 0 one lane a leaf, "
+                         "1 a lane pair a leaf, -1 the library default (pairs for a partial last generation)")
     a = ap.parse_args()
     from hydrabadger_amd import _lib, workload
     from hydrabadger_amd import broadcast as bc
@@ -68,8 +71,12 @@ def main():
 
         res = {"instances": B, "N": N, "P": P, "L": L}
         if "merkle" in whats:
-            res["merkle_ms"] = t(lambda: bc.merkle_build_batch(N, L, shards, levels, ctx=ctx, device=True,
-                                                                asynchronous=True))
+            for pm in [int(x) for x in a.pairs.split(",")]:
+                _lib.check(_lib.lib().hbg_test_set_merkle_pairs(ctx.h, pm))
+                key = "merkle_ms" if pm == -1 else f"merkle_pairs{pm}_ms"
+                res[key] = t(lambda: bc.merkle_build_batch(N, L, shards, levels, ctx=ctx, device=True,
+                                                           asynchronous=True))
+            _lib.check(_lib.lib().hbg_test_set_merkle_pairs(ctx.h, -1))
         if "encode" in whats:  # the two-launch schedule (rs_encode_const -> merkle_build)
             _lib.check(_lib.lib().hbg_test_set_rbc_fused(ctx.h, 0))
             res["encode_merkle_ms"] = t(lambda: bc.rbc_encode_merkle_batch(N, pay, plen, L, shards, levels, ctx=ctx,

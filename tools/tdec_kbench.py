@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cts", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--per-share", action="store_true",
+                    help="also time the HBG_VERIFY_PER_SHARE schedule (off: the PMC passes profile the batched call)")
     a = ap.parse_args()
     import bench
     from hydrabadger_amd import _lib
@@ -32,7 +34,7 @@ def main():
     torch.cuda.set_stream(st)
     ctx = _lib.Context(0)
     ctx.set_stream(st.cuda_stream)
-    print(json.dumps(bench.tdec_leg(ctx, dev, a.cts, a.reps)[0]), flush=True)
+    print(json.dumps(bench.tdec_leg(ctx, dev, a.cts, a.reps, per_share=a.per_share)[0]), flush=True)
     ctx.close()
 
 
