@@ -538,11 +538,16 @@ __global__ __launch_bounds__(256) void rs_plan(const uint8_t* __restrict__ prese
 // sends the launch's partial last generation of blocks there, as twice the
 // blocks of ~0.63 the duration, so it spreads over every CU instead of
 // adding a whole block duration on some of them.
-__global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
+// PAIRS: 0 one-lane blocks only; 1 lane-pair blocks only (no block prefetch,
+// 102 VGPRs: fewer than CUs' worth of blocks, latency-bound — 640 x N = 16
+// 0.75 -> 0.67 ms, 300 x N = 64 2.89 -> 2.62 ms against the prefetching pair
+// path, gpurun_out r06k2); 2 both, split at block b1 (the pairs prefetch)
+template <int PAIRS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PAIRS == 1 ? 5 : 1))) void merkle_build(const uint8_t* __restrict__ shards, uint64_t S, uint64_t L,
                                                     uint32_t N, uint32_t lpi, uint32_t nodes, uint64_t n,
                                                     uint8_t* __restrict__ levels, uint32_t b1, uint64_t n1) {
     extern __shared__ __attribute__((aligned(16))) uint32_t mlds[];
-    const bool pair = blockIdx.x >= b1;
+    const bool pair = PAIRS == 1 || (PAIRS == 2 && blockIdx.x >= b1);
     const uint32_t lanes = pair ? 2 * lpi : lpi;       // lanes per instance
     const uint32_t li = threadIdx.x / lanes, tl = threadIdx.x % lanes;
     const uint64_t inst = pair ? n1 + (uint64_t)(blockIdx.x - b1) * (256 / lanes) + li
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
         const uint32_t leaf = tl >> 1, half = tl & 1u;
         if (live && leaf < N) {
             uint32_t d[4];
-            sha3_256_aligned8_pair<true>(shards + (inst * N + leaf) * S, L, half, d);
+            sha3_256_aligned8_pair<PAIRS == 2>(shards + (inst * N + leaf) * S, L, half, d);
             uint32_t* g = reinterpret_cast<uint32_t*>(gout) + leaf * 8 + half;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -562,7 +567,7 @@ __global__ __launch_bounds__(256) void merkle_build(const uint8_t* __restrict__ 
                 g[2 * i] = d[i];
             }
         }
-    } else if (live && tl < N) {
+    } else if (PAIRS != 1 && live && tl < N) {
         const uint32_t leaf = tl;
         uint32_t d[8];
         sha3_256_aligned8<1, true>(shards + (inst * N + leaf) * S, L, d);
@@ -1575,8 +1580,13 @@ hipError_t launch_merkle_build(const uint8_t* shards, uint64_t S, uint64_t L, ui
     }
     const size_t lds = (size_t)ipb * nodes * 32;
     HBG_GRID_CHECK(b1 + b2, 256);
-    merkle_build<<<dim3((uint32_t)(b1 + b2)), dim3(256), lds, st>>>(shards, S, L, N, lpi, nodes, n, levels,
-                                                                   (uint32_t)b1, b1 * ipb);
+    const dim3 grid((uint32_t)(b1 + b2)), blk(256);
+    if (b2 == 0)
+        merkle_build<0><<<grid, blk, lds, st>>>(shards, S, L, N, lpi, nodes, n, levels, (uint32_t)b1, b1 * ipb);
+    else if (b1 == 0)
+        merkle_build<1><<<grid, blk, lds, st>>>(shards, S, L, N, lpi, nodes, n, levels, 0u, 0u);
+    else
+        merkle_build<2><<<grid, blk, lds, st>>>(shards, S, L, N, lpi, nodes, n, levels, (uint32_t)b1, b1 * ipb);
     return hipGetLastError();
 }
 

@@ -35,6 +35,12 @@ def build():
     # no divergent branch next to the products (bls.h fp_count): each lane adds 1, and the compiler's
     # wave-aggregating atomic optimizer (which would put the branch back) is off
     print(bv("fpcount", ["-DHBG_FP_COUNT", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]))
+    # the sources this instrumented library was built from: `run` stamps this
+    # digest (not the tree's), so a stale library never reads as measured at HEAD
+    sys.path.insert(0, ROOT)
+    from hydrabadger_amd.build import source_digest
+    with open(LIB + ".sha16", "w") as f:
+        f.write(source_digest() + "\n")
 
 
 def _report(lib) -> dict:
@@ -82,9 +88,12 @@ def run(n_ct: int, out: str, bad_rate: float = 0.01):
         return k, sum(v["per_share"] for v in k.values())
     dk, dtot = table(drv)
     vk, vtot = table(ver)
-    from hydrabadger_amd.build import source_digest
+    try:
+        built_from = open(LIB + ".sha16").read().strip()
+    except OSError:
+        built_from = None  # unknown sources: never matches HEAD
     res = {"source": f"tools/fpcount.py run --n-ct {n_ct} (instrumented build, HBG_FP_COUNT)",
-           "csrc_sha16": source_digest(),
+           "csrc_sha16": built_from,
            "shape": {"n_nodes": N, "t": t, "bad_rate": bad_rate, "n_ct": n_ct, "msg_len": ep.msg_len},
            "unit": "Fp multiplications + squarings (each 288 v_mad_u64_u32)",
            "per_share_total": dtot, "per_share_verify_total": vtot, "kernels": dk, "verify_kernels": vk,
