@@ -81,6 +81,16 @@ constexpr int kBufSc1 = 16;  // buffer aux bit: sc1 (served by L2, not the CU's 
 #define HBG_STORE_AUX 2
 #endif
 constexpr int kStoreAux = HBG_STORE_AUX;
+// ... and of the standalone encoders (rs_encode_const, rs_encode_missing):
+// nothing re-reads their rows in the same kernel, and the default policy
+// writes faster there (configs[1] rs_encode_const + merkle_build 2.60 ->
+// 2.43 ms, hbg_rs_encode 0.44 -> 0.35 ms, 8,192 x N = 64 two-launch 28.9 ->
+// 27.8 ms; the fused encoder with default-policy stores 26.6 -> 27.0 ms, so
+// it keeps nt: gpurun_out r06k4)
+#ifndef HBG_STORE_AUX_STANDALONE
+#define HBG_STORE_AUX_STANDALONE 0
+#endif
+constexpr int kStoreAuxStandalone = HBG_STORE_AUX_STANDALONE;
 
 // The rows of one encode: shard rows through `sh` (row J of the instance at
 // byte J*S + vsh of the resource; vsh = the lane's instance offset + 4t) and
@@ -109,7 +119,7 @@ __device__ __forceinline__ u32x2_a4 payload_window(const EncodeRows& r, uint32_t
     return u32x2_a4{v[0], v[1]};
 }
 
-template <int D, int Q, int MODE>
+template <int D, int Q, int MODE, int AUX>
 struct EncodeCtx {
     const EncodeRows& r;
     u32x2_a4 buf[kPrefetch];
@@ -141,7 +151,7 @@ struct EncodeCtx {
             w = buf[J % kPrefetch].x;
         }
         if constexpr (MODE != 0)
-            __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), kStoreAux);
+            __builtin_amdgcn_raw_buffer_store_b32(w, r.sh, r.vsh, (uint32_t)((uint64_t)J * r.S + 4 * r.p0), AUX);
         return w;
     }
 
@@ -177,7 +187,8 @@ struct EncodeCtx {
 // the missing parity rows; the present ones stay as received).
 template <int D, int Q, int MODE, bool RING = false, bool MASKED = false>
 __device__ __forceinline__ void encode_word(const EncodeRows& r) {
-    EncodeCtx<D, Q, MODE> cx{r, {}};
+    constexpr int AUX = RING ? kStoreAux : kStoreAuxStandalone;  // the fused encoder re-reads its rows
+    EncodeCtx<D, Q, MODE, AUX> cx{r, {}};
     uint32_t acc[Q];
 #pragma unroll
     for (int k = 0; k < Q; ++k) acc[k] = 0u;
@@ -189,7 +200,7 @@ __device__ __forceinline__ void encode_word(const EncodeRows& r) {
             if (!(((k < 64) ? (r.miss0 >> k) : (r.miss1 >> (k & 63))) & 1u)) continue;
         }
         __builtin_amdgcn_raw_buffer_store_b32(acc[k], r.sh, r.vsh, (uint32_t)((uint64_t)(D + k) * r.S + 4 * r.p0),
-                                              kStoreAux);
+                                              AUX);
         if constexpr (RING) r.ring[k * r.rdw] = acc[k];
     }
 }
