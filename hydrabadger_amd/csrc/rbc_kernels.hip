@@ -348,9 +348,16 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
     if (inst >= n) return;
     const uint32_t Q = N - D, qp = plan_qpad(Q);
     const uint8_t* pbase = plans + inst * plan_stride;
-    const CodePlan* plan = reinterpret_cast<const CodePlan*>(pbase);
-    if (plan->status != 0) return;
-    const uint32_t n_out = plan->n_out;
+    // the plan through the scalar cache (16-B aligned, wave-uniform): status,
+    // n_out and the row-index bytes as s_load_dword — vector loads of them sat
+    // on the critical path of every output row's store address
+    const cu32 pw = (cu32)pbase;
+    if ((int32_t)pw[0] != 0) return;  // CodePlan::status
+    const uint32_t n_out = pw[1];
+    constexpr uint32_t kInW = offsetof(CodePlan, in_idx) / 4, kOutW = offsetof(CodePlan, out_idx) / 4;
+    static_assert(offsetof(CodePlan, in_idx) % 4 == 0 && offsetof(CodePlan, out_idx) % 4 == 0, "dword-aligned");
+    auto in_row = [&](uint32_t j) { return (pw[kInW + (j >> 2)] >> (8 * (j & 3))) & 0xFFu; };
+    auto out_row = [&](uint32_t o) { return (pw[kOutW + (o >> 2)] >> (8 * (o & 3))) & 0xFFu; };
     const bool active = 4 * (uint64_t)p < L;
     const cu32 offs = (cu32)(pbase + plan_offs_at(D, Q));
     uint8_t* base = shards + inst * (uint64_t)N * S;
@@ -368,8 +375,7 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
         const uint32_t cnt = (n_out - o0) < (uint32_t)kGenericTile ? (n_out - o0) : (uint32_t)kGenericTile;
         const bool use_lds = cnt > (uint32_t)kMovrelSplit;
         for (uint32_t j = 0; j < D; ++j) {
-            const uint32_t w =
-                active ? reinterpret_cast<const uint32_t*>(base + (uint64_t)plan->in_idx[j] * S)[p] : 0u;
+            const uint32_t w = active ? reinterpret_cast<const uint32_t*>(base + (uint64_t)in_row(j) * S)[p] : 0u;
             const NibPair T = nib_tables(w);
             typedef uint32_t v16 __attribute__((ext_vector_type(16)));
             v16 tl, th;  // vector values: a dynamic uniform index lowers to v_movrels
@@ -407,8 +413,7 @@ __global__ __launch_bounds__(256) void rs_code_movrel(uint8_t* __restrict__ shar
         if (active) {
 #pragma unroll
             for (int o = 0; o < (int)kGenericTile; ++o)
-                if ((uint32_t)o < cnt)
-                    reinterpret_cast<uint32_t*>(base + (uint64_t)plan->out_idx[o0 + o] * S)[p] = acc[o];
+                if ((uint32_t)o < cnt) reinterpret_cast<uint32_t*>(base + (uint64_t)out_row(o0 + o) * S)[p] = acc[o];
         }
     }
 }
