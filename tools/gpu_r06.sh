@@ -60,6 +60,11 @@ for s in $STEPS; do
         TAG=$TAG/pmcrbc KB_ARGS="--what decode --dec-fused 1 --splits -1 --instances 8192 --reps 1" bash tools/pmc.sh \
             > "$OUT/pmcrbc.log" 2>&1 || { tail -30 "$OUT/pmcrbc.log"; exit 10; }
         OUT_ROOT="$OUT" python3 tools/pack_profiles.py rbc "gpurun_out/$TAG/pmcrbc/pmc/summary.txt" ;;
+    pmcrbc2)
+        # the two-launch schedule's kernels at the bench shape (after pmcrbc: updates its pmc_traffic.json)
+        TAG=$TAG/pmcrbc2 KB_ARGS="--what encode --instances 8192 --reps 1" bash tools/pmc.sh \
+            > "$OUT/pmcrbc2.log" 2>&1 || { tail -30 "$OUT/pmcrbc2.log"; exit 12; }
+        OUT_ROOT="$OUT" python3 tools/pack_profiles.py rbc2 "gpurun_out/$TAG/pmcrbc2/pmc/summary.txt" ;;
     pmctdec)
         TAG=$TAG/pmctdec KB_ARGS="--cts 100000 --reps 1" EXTRA_GROUPS="FETCH_SIZE WRITE_SIZE" bash tools/pmc_tdec.sh \
             > "$OUT/pmctdec.log" 2>&1 || { tail -30 "$OUT/pmctdec.log"; exit 11; }
