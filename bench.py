@@ -431,8 +431,8 @@ def tdec_leg(ctx, dev, n_ct: int, reps: int, seed: int = 1, bad_rate: float = 0.
            "n_ct": n_ct, "shares": n, "corrupted": int(ep.bad.sum()), "corrupted_by_kind": kinds,
            "faults_reported": int((oc == _lib.HBG_SHARE_FAULTY).sum().item()),
            "ok_bits_match": bits_ok, "outcomes_match": outcomes_ok, "plaintexts_match": pts_ok,
-           "batch_weights": {"bits": 127, "form": "a + b x^2, a odd, a and b the 64-bit halves of "
-                                                  "SHA3(K || batch digest || lane)",
+           "batch_weights": {"bits": 127, "form": "a + b|x| + c x^2 + d|x|^3, a odd, a..d the four 32-bit "
+                                                  "words of SHA3(K || batch digest || lane)",
                              "key": "32 secret bytes from getrandom(2) at hbg_init",
                              "soundness": "a (sub)batch check holding an invalid share passes with "
                                           "probability <= 2^-127",

@@ -996,7 +996,7 @@ int verify_shares_batched(hbg_ctx* c, uint32_t n_ct, CtTable& t, const uint8_t* 
         void* p;
         HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
         tbl = (uint32_t*)p;
-        HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream));
+        HBG_TRY(bls::launch_tdec_pk_table(n_pk, paff, tbl, c->stream, 1));
         HBG_DBG_STEP(c, "pk_table");
     }
     HBG_TRY(hipMemsetAsync(dok, 0, n, c->stream));
@@ -1476,7 +1476,7 @@ int hbg_sig_verify_shares(hbg_ctx* c, uint32_t n_doc, const uint8_t* doc, const 
         void* p;
         HBG_CHECK(scratch(c, 27, bls::tdec_pk_table_bytes(n_pk), &p));
         tbl = (uint32_t*)p;
-        HBG_TRY(bls::launch_tdec_pk_table(n_pk, pa, tbl, c->stream));
+        HBG_TRY(bls::launch_tdec_pk_table(n_pk, pa, tbl, c->stream, 0));
     }
     void *keys, *perm, *ta, *tb, *desc, *temp, *cnt;
     const size_t tb_bytes = bls::tdec_batch_temp_bytes(nn);

@@ -74,7 +74,10 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
                                     uint8_t* leaf_ok, const BatchKey& key, hipStream_t st,
                                     uint32_t* share_aff = nullptr);
 size_t tdec_pk_table_bytes(uint32_t n_pk);
-hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st);
+// layout 0: the coin shares' 64-bit-half weights; 1: the decryption shares'
+// four 32-bit quarters (windows 4..7 hold [|x|] PK)
+hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st,
+                                uint32_t layout);
 // Binary group testing (tdec_kernels.hip "batched share verification"):
 // round 0 over the batches, then kBinRounds rounds over BinItem lists (count:
 // a device word; items past next_cap hand their leaves to the per-share list).

@@ -1137,11 +1137,13 @@ __global__ __launch_bounds__(256) void tdec_index_sanitize(uint64_t n, const uin
 // verify_decryption_share for many shares of ONE ciphertext c shares (H, W):
 // e(S_i, H) == e(PK_i, W) for all i in a batch  <=  e(sum r_i S_i, H) ==
 // e(sum r_i PK_i, W) with secret 127-bit weights r_i (Bellare-Garay-Rabin
-// small-exponent batch test).  r_i = a_i + b_i x^2 with a_i (odd) and b_i the
-// two 64-bit halves of SHA3(K || D || i): K is the context's secret batch key
-// (32 bytes from getrandom at hbg_init, never exposed), D a digest of the whole
-// batch.  The 2^127 (a, b) pairs are 2^127 distinct integers below the group
-// order (a < 2^64 < x^2; r < 2^193), so for any batch holding an invalid share
+// small-exponent batch test).  r_i = a + b|x| + c x^2 + d|x|^3 with a (odd),
+// b, c, d the four 32-bit words of SHA3(K || D || i) (w4_weight; the coin
+// shares' leaves use r_i = a + b x^2 with the two 64-bit halves instead,
+// batch_weight): K is the context's secret batch key (32 bytes from getrandom
+// at hbg_init, never exposed), D a digest of the whole batch.  Either way the
+// 2^127 tuples are 2^127 distinct integers below the group order (every digit
+// is below its base: a < 2^64 < x^2, resp. 32-bit quarters < |x|), so for any batch holding an invalid share
 // and any fixed choice of the other weights at most one value of r_i makes the
 // weighted product 1: a (sub)tree holding an invalid share passes with
 // probability <= 2^-127, and no sender can grind shares against the weights
@@ -1236,19 +1238,30 @@ BD G1 g1_shfl_xor(const G1& p, int m) {
 }
 
 // Fixed-base tables of the public key shares for the batch weights:
-// tbl[pk][w][v] = affine [v * 2^(8w)] PK_pk, v in 1..255, w in 0..7 (v = 0
-// unused), so [a] PK for a 64-bit weight half is 8 mixed additions, no
-// doublings (the b half reads the same entries through (beta x, -y)).
+// tbl[pk][w][v] (v in 1..255; v = 0 unused), affine.  Layout 0 (the coin
+// shares' 64-bit halves a + b x^2): [v 2^(8w)] PK for w in 0..7, so [a] PK is
+// 8 mixed additions, no doublings (the b half reads the same entries through
+// (beta x, -y)).  Layout 1 (the decryption shares' four 32-bit quarters
+// a + b|x| + c x^2 + d|x|^3, w4_weight): [v 2^(8w)] PK for w in 0..3 and
+// [v 2^(8(w - 4))] ([|x|] PK) for w in 4..7 — 16 mixed additions either way.
 constexpr uint32_t kPkTblWords = 8 * 256 * 24;
 TDEC_KERNEL void tdec_pk_table(uint32_t n_pk, const uint32_t* __restrict__ pk_aff,
-                                                    uint32_t* __restrict__ tbl) {
+                                                    uint32_t* __restrict__ tbl, uint32_t layout) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // (pk, w, v)
     if (i >= n_pk * 2048u) return;
     const uint32_t pk = i >> 11, w = (i >> 8) & 7u, v = i & 255u;
     const uint32_t* pa = pk_aff + 32ull * pk;
     uint32_t* o = tbl + (uint64_t)pk * kPkTblWords + (uint64_t)(w * 256 + v) * 24;
     if (v == 0 || pa[24] != 0) return;
-    const G1A r = g1_to_affine(g1_mul_u64(load_fp(pa), load_fp(pa + 12), (uint64_t)v << (8 * w)));
+    const Fp px = load_fp(pa), py = load_fp(pa + 12);
+    G1 e;
+    if (layout == 1 && w >= 4) {
+        // [|x|] PK != O for PK in G1 (pk_prepare checked the subgroup)
+        e = g1_mul_u64_jac(g1_mul_u64(px, py, kBlsX), (uint64_t)v << (8 * (w - 4)));
+    } else {
+        e = g1_mul_u64(px, py, (uint64_t)v << (8 * w));
+    }
+    const G1A r = g1_to_affine(e);
     store_fp(o, r.x);
     store_fp(o + 12, r.y);
 }
@@ -1305,6 +1318,115 @@ BD void batch_weight(const BatchKey& key, const uint8_t* D, uint32_t lane, uint6
     a |= 1u;
 }
 
+// ---- the decryption shares' weights: four 32-bit quarters -------------------
+// r = a + b|x| + c x^2 + d|x|^3 (a odd), a, b, c, d the four LE 32-bit words of
+// SHA3(K || D || lane) — the same key, digest and derivation as batch_weight.
+// 2^127 distinct integers (the quarters are below |x| > 2^63, so the base-|x|
+// representation is unique) below 2^224 < the group order, nonzero (a odd).
+// On G1, [x^2]P = -phi(P) = (beta x, -y) and [|x|^3]P = -phi([|x|]P), and
+// [|x|]P is the subgroup check's intermediate (g1_subgroup_t1): the four
+// points cost nothing extra, and r P is two 32-step joint double-and-adds
+// sharing their 32 doublings (g1_mul_w4) instead of one 64-step one.
+struct W4 {
+    uint32_t a, b, c, d;
+};
+BD W4 w4_weight(const BatchKey& key, const uint8_t* D, uint32_t lane) {
+    uint8_t m[68], dg[32];
+    for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 4; ++j) m[4 * i + j] = (uint8_t)(key.w[i] >> (8 * j));
+    for (int i = 0; i < 32; ++i) m[32 + i] = D[i];
+    for (int i = 0; i < 4; ++i) m[64 + i] = (uint8_t)(lane >> (8 * i));
+    sha3_bytes(m, 68, dg);
+    auto word = [&](int k) {
+        return (uint32_t)dg[4 * k] | ((uint32_t)dg[4 * k + 1] << 8) | ((uint32_t)dg[4 * k + 2] << 16) |
+               ((uint32_t)dg[4 * k + 3] << 24);
+    };
+    return {word(0) | 1u, word(1), word(2), word(3)};
+}
+
+// P in G1 (g1_in_subgroup's test, phi(P) == [-x^2]P), keeping T1 = [|x|]P
+// (Jacobian, Z != 0 when the test passes) for g1_mul_w4.
+BD bool g1_subgroup_t1(const Fp& px, const Fp& py, G1& t1) {
+    t1 = g1_mul_u64(px, py, kBlsX);
+    if (fp_is_zero(t1.z)) return false;
+    const G1 u = g1_mul_u64_jac(t1, kBlsX);
+    if (fp_is_zero(u.z)) return false;
+    const Fp z2 = fp_sqr(u.z), z3 = fp_mul(z2, u.z);
+    return fp_eq(fp_mul(fp_mul(px, fp_const(kBeta)), z2), u.x) && fp_eq(fp_mul(py, z3), fp_neg(u.y));
+}
+
+// [a + b|x| + c x^2 + d|x|^3] P for P in G1 (affine, not infinity) and
+// T1 = [|x|]P (Jacobian): pair A = (P, -phi P, their sum) takes the (a, c)
+// bits, pair B = (T1, -phi T1, their sum) the (b, d) bits; per step one
+// doubling and two branch-free mixed additions.  All six addends are put on
+// one isomorphic curve E_W: y^2 = x^3 + 4 W^6, W = Z_A Z_B Z_1 (a Jacobian
+// (X, Y, Z) is the affine (X (W/Z)^2, Y (W/Z)^3) there; the a = 0 formulas
+// never read the constant), and the result maps back as (X', Y', Z' W).
+// Z_A, Z_B, Z_1 != 0 for P != O in G1 (phi has no eigenvalue -1 there).
+BD G1 g1_mul_w4(const Fp& px, const Fp& py, const G1& t1, const W4& k) {
+    const Fp bx = fp_mul(px, fp_const(kBeta));
+    const G1 sa = g1_add_mixed({px, py, fp_one()}, bx, fp_neg(py));           // P - phi P
+    const G1 tc = {fp_mul(t1.x, fp_const(kBeta)), fp_neg(t1.y), t1.z};        // -phi T1
+    const G1 sb = g1_add(t1, tc);                                              // T1 - phi T1
+    Fp zab, zb1, za1;
+    fp_mul3(zab, zb1, za1, sa.z, sb.z, sb.z, t1.z, sa.z, t1.z);
+    const Fp W = fp_mul(zab, t1.z);                                            // lambda of P, -phi P
+    // lambda^2, lambda^3 of P (W), T1 (zab), A (zb1), B (za1)
+    Fp w2, t2, a2, b2, w3, t3, a3, b3;
+    fp_mul2(w2, t2, W, W, zab, zab);
+    fp_mul2(a2, b2, zb1, zb1, za1, za1);
+    fp_mul2(w3, t3, w2, W, t2, zab);
+    fp_mul2(a3, b3, a2, zb1, b2, za1);
+    Fp pxw, pyw, ax, ay, tx, ty, bxw, byw;
+    fp_mul2(pxw, pyw, px, w2, py, w3);
+    fp_mul2(ax, ay, sa.x, a2, sa.y, a3);
+    fp_mul2(tx, ty, t1.x, t2, t1.y, t3);
+    fp_mul2(bxw, byw, sb.x, b2, sb.y, b3);
+    const Fp pcx = fp_mul(pxw, fp_const(kBeta));  // -phi P on E_W: (pcx, -pyw)
+    const Fp tcx = fp_mul(tx, fp_const(kBeta));   // -phi T1 on E_W: (tcx, -ty)
+    G1 r = {fp_one(), fp_one(), fp_zero()};
+#pragma unroll 1
+    for (int bit = 31; bit >= 0; --bit) {
+        r = g1_dbl(r);
+        // the y of -phi is negated at use (two fewer 12-word values live)
+        const bool ea = (k.a >> bit) & 1u, ec = (k.c >> bit) & 1u;
+        const G1 s1 = g1_add_mixed(r, ea ? (ec ? ax : pxw) : pcx, ea ? (ec ? ay : pyw) : fp_neg(pyw));
+        if (ea || ec) r = s1;
+        const bool eb = (k.b >> bit) & 1u, ed = (k.d >> bit) & 1u;
+        const G1 s2 = g1_add_mixed(r, eb ? (ed ? bxw : tx) : tcx, eb ? (ed ? byw : ty) : fp_neg(ty));
+        if (eb || ed) r = s2;
+    }
+    return {r.x, r.y, fp_mul(r.z, W)};
+}
+
+// r PK from the key's layout-1 table (tdec_pk_table): the a and c quarters
+// from windows 0..3 (c through (beta x, -y) = [x^2]), b and d from windows
+// 4..7 ([|x|] PK; d through (beta x, -y)): 16 mixed additions, no doublings.
+BD G1 pk_tbl_mul_w4(const uint32_t* t, const W4& k) {
+    G1 B = {fp_one(), fp_one(), fp_zero()};
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t va = (k.a >> (8 * w)) & 255u, vc = (k.c >> (8 * w)) & 255u;
+        const uint32_t vb = (k.b >> (8 * w)) & 255u, vd = (k.d >> (8 * w)) & 255u;
+        if (va) {
+            const uint32_t* e = t + (w * 256 + va) * 24;
+            B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+        }
+        if (vc) {
+            const uint32_t* e = t + (w * 256 + vc) * 24;
+            B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
+        }
+        if (vb) {
+            const uint32_t* e = t + ((4 + w) * 256 + vb) * 24;
+            B = g1_add_mixed(B, load_fp(e), load_fp(e + 12));
+        }
+        if (vd) {
+            const uint32_t* e = t + ((4 + w) * 256 + vd) * 24;
+            B = g1_add_mixed(B, fp_mul(load_fp(e), fp_const(kBeta)), fp_neg(load_fp(e + 12)));
+        }
+    }
+    return B;
+}
+
 // [a + b x^2] PK from the key's fixed-base table (windows 0..7 of both halves;
 // the b half through (beta x, -y)): 16 mixed additions, no doublings.
 BD G1 pk_tbl_mul_ab64(const uint32_t* t, uint64_t a, uint64_t b) {
@@ -1353,7 +1475,9 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
     const bool real_ct = d.ct < n_ct;  // the sentinel batch (out-of-range indices) reads no U
     bool valid = in && ct_status[d.ct] == 0 && pk_status[pk] == 0;
     G1A s;
-    if (valid) valid = g1_decompress(share48 + 48ull * k, s, true);
+    G1 t1;  // [|x|] S, the subgroup check's intermediate (the weight's b, d points)
+    if (valid) valid = g1_decompress(share48 + 48ull * k, s, false);
+    if (valid && !s.inf) valid = g1_subgroup_t1(s.x, s.y, t1);
     if (valid && share_aff) store_aff(share_aff + (uint64_t)kAffWords * k, s);  // for the combine
     // Weights: r_i from SHA3(K || D || i) with D = SHA3(d_0 || ...) over the
     // leaf digests d_i = SHA3(U || S_i || pk_i) — secret (K) and bound to the
@@ -1370,15 +1494,19 @@ TDEC_KERNEL void tdec_batch_leaves(uint32_t cap, const uint32_t* __restrict__ nb
     __syncthreads();
     G1 A = {fp_one(), fp_one(), fp_zero()}, B = A;
     if (valid) {
-        // weight r_i = a + b x^2 (a odd: nonzero); S_i and pk_i are in G1
-        // (decoded with the subgroup check), where [x^2]P = (beta px, -py)
-        uint64_t ra, rb;
-        batch_weight(key, sBatch, lane, ra, rb);
-        if (!s.inf) A = g1_mul_ab64(s.x, s.y, ra, rb);
+        // weight r_i = a + b|x| + c x^2 + d|x|^3 (w4_weight; a odd: nonzero);
+        // S_i and pk_i are in G1 (subgroup-checked)
+        const W4 w = w4_weight(key, sBatch, lane);
+        if (!s.inf) A = g1_mul_w4(s.x, s.y, t1, w);
         const uint32_t* pa = pk_aff + 32ull * pk;
-        if (pa[24] == 0)
-            B = pk_tbl ? pk_tbl_mul_ab64(pk_tbl + (uint64_t)pk * kPkTblWords, ra, rb)
-                       : g1_mul_ab64(load_fp(pa), load_fp(pa + 12), ra, rb);
+        if (pa[24] == 0) {
+            if (pk_tbl) {
+                B = pk_tbl_mul_w4(pk_tbl + (uint64_t)pk * kPkTblWords, w);
+            } else {
+                const Fp px = load_fp(pa), py = load_fp(pa + 12);
+                B = g1_mul_w4(px, py, g1_mul_u64(px, py, kBlsX), w);
+            }
+        }
     }
     leaf_ok[(uint64_t)b * kBatchShares + lane] = valid ? 1 : 0;
     // the binary tree's left nodes (slot h / 2) and the root (slot 0): the
@@ -3040,10 +3168,11 @@ hipError_t launch_tdec_batch_leaves(uint32_t nb_max, const uint32_t* nb_dev, uin
 
 size_t tdec_pk_table_bytes(uint32_t n_pk) { return 4ull * kPkTblWords * n_pk; }
 
-hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st) {
+hipError_t launch_tdec_pk_table(uint32_t n_pk, const uint32_t* pk_aff, uint32_t* tbl, hipStream_t st,
+                                uint32_t layout) {
     HBG_COUNT_MARK("tdec_pk_table", st);
     if (n_pk == 0) return hipSuccess;
-    tdec_pk_table<<<dim3((n_pk * 2048u + 63) / 64), dim3(64), 0, st>>>(n_pk, pk_aff, tbl);
+    tdec_pk_table<<<dim3((n_pk * 2048u + 63) / 64), dim3(64), 0, st>>>(n_pk, pk_aff, tbl, layout);
     return hipGetLastError();
 }
 

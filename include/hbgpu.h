@@ -205,8 +205,10 @@ int hbg_rbc_decode(hbg_ctx *ctx, uint32_t N, uint64_t shard_len, uint8_t *shards
  *    shares; smaller calls run per share.  Every 0 bit is the crate's per-share
  *    verdict.  A 1 bit comes from a passing (sub)batch and equals the crate's
  *    bool except with probability <= 2^-127 per (sub)batch check that holds an
- *    invalid share: the weights are 127-bit (a + b x^2, a odd, a and b 64-bit)
- *    and derived from a secret 32-byte key drawn from getrandom(2) at hbg_init
+ *    invalid share: the weights take 2^127 distinct values (decryption shares:
+ *    a + b|x| + c x^2 + d|x|^3, a..d 32-bit; coin shares: a + b x^2, a and b
+ *    64-bit; a odd) and are derived from a secret 32-byte key drawn from
+ *    getrandom(2) at hbg_init
  *    and never exposed, so a sender can neither predict nor grind them.
  * Returns HBG_E_ARG for any other mode. */
 #define HBG_VERIFY_BATCHED 0
