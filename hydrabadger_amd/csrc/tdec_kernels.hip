@@ -1388,12 +1388,15 @@ BD G1 g1_mul_w4(const Fp& px, const Fp& py, const G1& t1, const W4& k) {
 #pragma unroll 1
     for (int bit = 31; bit >= 0; --bit) {
         r = g1_dbl(r);
-        // the y of -phi is negated at use (two fewer 12-word values live)
+        // the y of -phi is the selected y negated per step (a select of a
+        // bit-dependent value: not hoisted, two fewer 12-word values live)
         const bool ea = (k.a >> bit) & 1u, ec = (k.c >> bit) & 1u;
-        const G1 s1 = g1_add_mixed(r, ea ? (ec ? ax : pxw) : pcx, ea ? (ec ? ay : pyw) : fp_neg(pyw));
+        const Fp ya = (ea && ec) ? ay : pyw;
+        const G1 s1 = g1_add_mixed(r, ea ? (ec ? ax : pxw) : pcx, ea ? ya : fp_neg(ya));
         if (ea || ec) r = s1;
         const bool eb = (k.b >> bit) & 1u, ed = (k.d >> bit) & 1u;
-        const G1 s2 = g1_add_mixed(r, eb ? (ed ? bxw : tx) : tcx, eb ? (ed ? byw : ty) : fp_neg(ty));
+        const Fp yb = (eb && ed) ? byw : ty;
+        const G1 s2 = g1_add_mixed(r, eb ? (ed ? bxw : tx) : tcx, eb ? yb : fp_neg(yb));
         if (eb || ed) r = s2;
     }
     return {r.x, r.y, fp_mul(r.z, W)};
