@@ -285,6 +285,7 @@ def test_batched_verify_equals_per_share(bad_rate, seed):
     junk = bytearray(items[5][0]); junk[0] &= 0x7F                            # invalid encoding
     items.append((bytes(junk), 3, 5)); expect.append(0)
     items.append((B.g1_compress(B.G1), 7, 9)); expect.append(0)               # valid point, wrong share
+    items.append((bytes([0xC0]) + bytes(47), 11, 3)); expect.append(0)          # identity share (in G1, wrong)
     order = rng.permutation(len(items))
     items = [items[k] for k in order]
     expect = np.array([expect[k] for k in order], np.uint8)
